@@ -1,0 +1,72 @@
+"""Native build of the MI355X engine (in-tree, no JIT cache).
+
+* ``libalaya_hip.so``  -- the C-ABI library (include/alaya_hip.h): HIP kernels for gfx950 + host C++
+  (graph builder, on-disk formats), compiled with hipcc --offload-arch=gfx950.
+* ``_alayalitepy*.so`` -- pybind11 module mirroring the reference binding, linked to the library.
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU-only build container too.
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sysconfig
+
+import pybind11
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+INCLUDE = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("ALAYA_OFFLOAD_ARCH", "gfx950")
+
+LIB = os.path.join(HERE, "libalaya_hip.so")
+EXT = os.path.join(HERE, "_alayalitepy" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+LIB_SOURCES = ["search_kernels.hip", "capi.cpp", "hnsw_build.cpp"]
+LIB_HEADERS = ["search_kernels.h", "hnsw_build.h", "host_distance.h"]
+EXT_SOURCES = ["pybind_module.cpp"]
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build(force: bool = False, verbose: bool = False) -> tuple[str, str]:
+    lib_deps = [os.path.join(CSRC, f) for f in LIB_SOURCES + LIB_HEADERS] + [os.path.join(INCLUDE, "alaya_hip.h")]
+    if force or _newer(LIB, lib_deps):
+        objs = []
+        for src in LIB_SOURCES:
+            obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
+            flags = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-pthread",
+                     f"-I{INCLUDE}", "-c", os.path.join(CSRC, src), "-o", obj]
+            if src.endswith(".hip"):
+                flags[1:1] = ["-x", "hip", f"--offload-arch={ARCH}"]
+            _run(flags, verbose)
+            objs.append(obj)
+        _run([HIPCC, "-shared", "-fPIC", "-pthread", "-o", LIB] + objs + ["-lamdhip64"], verbose)
+        for o in objs:
+            os.remove(o)
+    ext_deps = [os.path.join(CSRC, f) for f in EXT_SOURCES + ["host_distance.h"]] + [LIB]
+    if force or _newer(EXT, ext_deps):
+        py_inc = sysconfig.get_paths()["include"]
+        _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off", "-Wall", "-fvisibility=hidden",
+              f"-I{pybind11.get_include()}", f"-I{py_inc}", f"-I{INCLUDE}",
+              os.path.join(CSRC, "pybind_module.cpp"), "-o", EXT, f"-L{HERE}", "-lalaya_hip",
+              "-Wl,-rpath,$ORIGIN"], verbose)
+    return LIB, EXT
+
+
+if __name__ == "__main__":
+    build(force=True, verbose=True)

@@ -1,0 +1,471 @@
+// C-ABI implementation (include/alaya_hip.h): device-resident index state, uploads, launches.
+#include "../../include/alaya_hip.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hnsw_build.h"
+#include "search_kernels.h"
+
+using alaya_amd::HostGraph;
+using alaya_amd::SearchParams;
+
+struct alaya_graph {
+  HostGraph g;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct ArgError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct DeviceError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw DeviceError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename F>
+int guarded(F &&f) {
+  try {
+    f();
+    return ALAYA_OK;
+  } catch (const ArgError &e) {
+    g_last_error = e.what();
+    return ALAYA_ERR_ARG;
+  } catch (const DeviceError &e) {
+    g_last_error = e.what();
+    return ALAYA_ERR_DEVICE;
+  } catch (const std::exception &e) {
+    g_last_error = e.what();
+    return ALAYA_ERR_RUNTIME;
+  }
+}
+
+// Grow-only device buffer.
+struct DevBuf {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+  void reserve(size_t n) {
+    if (n <= bytes) return;
+    release();
+    hip_check(hipMalloc(&ptr, std::max<size_t>(n, 256)), "hipMalloc");
+    bytes = std::max<size_t>(n, 256);
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T *as() const {
+    return static_cast<T *>(ptr);
+  }
+  ~DevBuf() { release(); }
+};
+
+uint32_t round_up32(uint32_t d) { return (d + 31u) / 32u * 32u; }
+
+uint32_t ceil_log2(uint64_t v) {
+  uint32_t l = 0;
+  while ((1ull << l) < v) ++l;
+  return l;
+}
+
+}  // namespace
+
+struct alaya_index {
+  int device = 0;
+  std::mutex mu;
+  // base
+  uint64_t n = 0;
+  uint32_t dim = 0, stride = 0;
+  int metric = ALAYA_METRIC_L2;
+  DevBuf base, valid;
+  bool has_valid = false;
+  // graph
+  bool has_graph = false;
+  uint32_t R = 0, upper_R = 0, ep = 0, n_eps = 0;
+  bool has_overlay = false, dedup = false;
+  DevBuf l0, levels, upper_off, upper_edges, eps;
+  uint64_t graph_n = 0;
+  // scratch
+  DevBuf work, overflow, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
+  uint32_t hash_log2_override = 0;
+  int num_cus = 0;
+  hipStream_t stream = nullptr;
+  uint64_t device_bytes() const {
+    return base.bytes + valid.bytes + l0.bytes + levels.bytes + upper_off.bytes +
+           upper_edges.bytes + eps.bytes + overflow.bytes;
+  }
+};
+
+namespace {
+
+void set_device(const alaya_index *ix) { hip_check(hipSetDevice(ix->device), "hipSetDevice"); }
+
+SearchParams base_params(alaya_index *ix) {
+  SearchParams p{};
+  p.base = ix->base.as<float>();
+  p.n = ix->n;
+  p.dim = ix->dim;
+  p.stride = ix->stride;
+  p.valid = ix->has_valid ? ix->valid.as<uint32_t>() : nullptr;
+  p.ip = ix->metric != ALAYA_METRIC_L2;
+  return p;
+}
+
+uint32_t auto_hash_log2(uint32_t ef) {
+  return std::min<uint32_t>(14, std::max<uint32_t>(11, ceil_log2(32ull * ef)));
+}
+
+void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t ef,
+               uint32_t *d_ids, float *d_dists, uint32_t *d_cnt, hipStream_t stream) {
+  if (!ix->base.ptr) throw ArgError("index has no base vectors");
+  if (!ix->has_graph) throw ArgError("index has no graph");
+  if (ef == 0) throw ArgError("ef must be >= 1");
+  if (k == 0 || nq == 0) return;
+  if (ix->graph_n > ix->n) throw ArgError("graph has more nodes than base vectors");
+  SearchParams p = base_params(ix);
+  p.l0 = ix->l0.as<uint32_t>();
+  p.R = ix->R;
+  p.dedup_edges = ix->dedup;
+  p.levels = ix->has_overlay ? ix->levels.as<uint32_t>() : nullptr;
+  p.upper_off = ix->upper_off.as<uint64_t>();
+  p.upper_edges = ix->upper_edges.as<uint32_t>();
+  p.upper_R = ix->upper_R;
+  p.ep = ix->ep;
+  p.eps = ix->eps.as<uint32_t>();
+  p.n_eps = ix->n_eps;
+  p.queries = d_q;
+  p.nq = nq;
+  p.q_stride = ix->dim;
+  p.k = k;
+  p.ef = ef;
+  p.out_ids = d_ids;
+  p.out_dists = d_dists;
+  p.out_counters = d_cnt;
+  p.hash_log2 = ix->hash_log2_override ? ix->hash_log2_override : auto_hash_log2(ef);
+  const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2);
+  if (lds > 160 * 1024) throw ArgError("ef / dim too large for the LDS budget");
+  int per_cu = 0;
+  hip_check(alaya_amd::search_occupancy(p, lds, &per_cu), "occupancy");
+  per_cu = std::max(1, per_cu);
+  const uint64_t grid64 = std::min<uint64_t>(nq, static_cast<uint64_t>(per_cu) * ix->num_cus);
+  const int grid = static_cast<int>(std::max<uint64_t>(1, grid64));
+  const uint64_t words = (ix->n + 31) / 32;
+  ix->overflow.reserve(static_cast<size_t>(grid) * words * 4);
+  ix->work.reserve(4);
+  p.overflow_bits = ix->overflow.as<uint32_t>();
+  p.work_counter = ix->work.as<uint32_t>();
+  hip_check(hipMemsetAsync(p.work_counter, 0, 4, stream), "hipMemsetAsync");
+  hip_check(alaya_amd::launch_search(p, grid, lds, stream), "search launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *alaya_last_error(void) { return g_last_error.c_str(); }
+
+int alaya_device_count(int *count) {
+  return guarded([&] {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+  });
+}
+
+// ---- graphs ---------------------------------------------------------------------------------
+int alaya_graph_build_hnsw(const float *data, uint64_t n, uint32_t dim, int metric, uint32_t R,
+                           uint32_t ef_construction, uint32_t num_threads, uint64_t seed,
+                           alaya_graph **out) {
+  return guarded([&] {
+    if (!out || (n && !data) || dim == 0) throw ArgError("invalid arguments");
+    if (n >= (1ull << 31)) throw ArgError("ids must stay below 2^31 (LinearPool checked bit)");
+    auto g = std::make_unique<alaya_graph>();
+    g->g = alaya_amd::build_hnsw(data, n, dim, metric, R, ef_construction, num_threads, seed);
+    *out = g.release();
+  });
+}
+
+int alaya_graph_load(const char *path, int id_bytes, alaya_graph **out) {
+  return guarded([&] {
+    if (!out || !path) throw ArgError("invalid arguments");
+    auto g = std::make_unique<alaya_graph>();
+    g->g = alaya_amd::load_graph(path, id_bytes);
+    *out = g.release();
+  });
+}
+
+int alaya_graph_save(const alaya_graph *g, const char *path, int id_bytes, uint64_t capacity) {
+  return guarded([&] {
+    if (!g || !path) throw ArgError("invalid arguments");
+    alaya_amd::save_graph(g->g, path, id_bytes, capacity);
+  });
+}
+
+int alaya_graph_info(const alaya_graph *g, uint64_t *n, uint32_t *R, int *has_overlay,
+                     uint32_t *upper_R, uint32_t *ep, uint32_t *max_level,
+                     uint64_t *n_upper_edges, uint32_t *n_eps) {
+  return guarded([&] {
+    if (!g) throw ArgError("null graph");
+    if (n) *n = g->g.n;
+    if (R) *R = g->g.R;
+    if (has_overlay) *has_overlay = g->g.has_overlay ? 1 : 0;
+    if (upper_R) *upper_R = g->g.upper_R;
+    if (ep) *ep = g->g.ep;
+    if (max_level) *max_level = g->g.max_level();
+    if (n_upper_edges) *n_upper_edges = g->g.upper_edges.size();
+    if (n_eps) *n_eps = static_cast<uint32_t>(g->g.eps.size());
+  });
+}
+
+int alaya_graph_export(const alaya_graph *g, uint32_t *l0, uint32_t *levels, uint64_t *upper_off,
+                       uint32_t *upper_edges, uint32_t *eps) {
+  return guarded([&] {
+    if (!g) throw ArgError("null graph");
+    const HostGraph &h = g->g;
+    if (l0) std::memcpy(l0, h.l0.data(), h.l0.size() * 4);
+    if (levels && !h.levels.empty()) std::memcpy(levels, h.levels.data(), h.levels.size() * 4);
+    if (upper_off && !h.upper_off.empty()) std::memcpy(upper_off, h.upper_off.data(), h.upper_off.size() * 8);
+    if (upper_edges && !h.upper_edges.empty())
+      std::memcpy(upper_edges, h.upper_edges.data(), h.upper_edges.size() * 4);
+    if (eps && !h.eps.empty()) std::memcpy(eps, h.eps.data(), h.eps.size() * 4);
+  });
+}
+
+int alaya_graph_import(uint64_t n, uint32_t R, const uint32_t *l0, const uint32_t *levels,
+                       const uint64_t *upper_off, const uint32_t *upper_edges,
+                       uint64_t n_upper_edges, uint32_t upper_R, uint32_t ep, const uint32_t *eps,
+                       uint32_t n_eps, alaya_graph **out) {
+  return guarded([&] {
+    if (!out || (n && !l0) || R == 0 || R > 64) throw ArgError("invalid graph arrays (R must be 1..64)");
+    auto g = std::make_unique<alaya_graph>();
+    HostGraph &h = g->g;
+    h.n = n;
+    h.R = R;
+    h.l0.assign(l0, l0 + n * R);
+    if (levels) {
+      if (!upper_off || (n_upper_edges && !upper_edges) || upper_R == 0 || upper_R > 64)
+        throw ArgError("invalid overlay arrays (upper_R must be 1..64)");
+      if (n && ep >= n) throw ArgError("entry point out of range");
+      h.has_overlay = true;
+      h.levels.assign(levels, levels + n);
+      h.upper_off.assign(upper_off, upper_off + n);
+      h.upper_edges.assign(upper_edges, upper_edges + n_upper_edges);
+      h.upper_R = upper_R;
+      h.ep = ep;
+      for (uint64_t i = 0; i < n; ++i)
+        if (h.levels[i] && h.upper_off[i] + static_cast<uint64_t>(h.levels[i]) * upper_R > n_upper_edges)
+          throw ArgError("upper_off/levels exceed upper_edges");
+    } else {
+      if (n_eps == 0 && n) throw ArgError("graph without overlay needs entry points");
+      h.eps.assign(eps, eps + n_eps);
+    }
+    *out = g.release();
+  });
+}
+
+void alaya_graph_free(alaya_graph *g) { delete g; }
+
+// ---- device index ----------------------------------------------------------------------------
+int alaya_index_create(int device, alaya_index **out) {
+  return guarded([&] {
+    if (!out) throw ArgError("null out");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+      throw DeviceError("no HIP device available (the MI355X search path has no CPU fallback)");
+    if (device < 0 || device >= count) throw ArgError("device ordinal out of range");
+    auto ix = std::make_unique<alaya_index>();
+    ix->device = device;
+    set_device(ix.get());
+    hipDeviceProp_t prop;
+    hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+    ix->num_cus = prop.multiProcessorCount;
+    hip_check(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking), "hipStreamCreate");
+    *out = ix.release();
+  });
+}
+
+void alaya_index_destroy(alaya_index *ix) {
+  if (!ix) return;
+  (void)hipSetDevice(ix->device);
+  if (ix->stream) (void)hipStreamDestroy(ix->stream);
+  delete ix;
+}
+
+int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_t dim, int metric,
+                         const uint8_t *valid_bitmap) {
+  return guarded([&] {
+    if (!ix || (n && !rows) || dim == 0) throw ArgError("invalid arguments");
+    if (metric < ALAYA_METRIC_L2 || metric > ALAYA_METRIC_COS) throw ArgError("unknown metric");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    const uint32_t stride = round_up32(dim);
+    ix->base.release();
+    ix->base.reserve(std::max<uint64_t>(n, 1) * stride * 4);
+    if (n) {
+      hip_check(hipMemset2DAsync(ix->base.ptr, static_cast<size_t>(stride) * 4, 0,
+                                 static_cast<size_t>(stride) * 4, n, ix->stream), "memset");
+      hip_check(hipMemcpy2DAsync(ix->base.ptr, static_cast<size_t>(stride) * 4, rows,
+                                 static_cast<size_t>(dim) * 4, static_cast<size_t>(dim) * 4, n,
+                                 hipMemcpyHostToDevice, ix->stream), "upload base");
+    }
+    ix->has_valid = valid_bitmap != nullptr;
+    ix->valid.release();
+    if (valid_bitmap) {
+      const size_t words = (n + 31) / 32;
+      std::vector<uint32_t> w(std::max<size_t>(words, 1), 0);
+      std::memcpy(w.data(), valid_bitmap, (n + 7) / 8);
+      ix->valid.reserve(w.size() * 4);
+      hip_check(hipMemcpyAsync(ix->valid.ptr, w.data(), w.size() * 4, hipMemcpyHostToDevice,
+                               ix->stream), "upload bitmap");
+      hip_check(hipStreamSynchronize(ix->stream), "sync");
+    }
+    hip_check(hipStreamSynchronize(ix->stream), "sync");
+    ix->n = n;
+    ix->dim = dim;
+    ix->stride = stride;
+    ix->metric = metric;
+    ix->overflow.release();
+  });
+}
+
+int alaya_index_set_graph(alaya_index *ix, const alaya_graph *g) {
+  return guarded([&] {
+    if (!ix || !g) throw ArgError("invalid arguments");
+    const HostGraph &h = g->g;
+    if (h.R == 0 || h.R > 64) throw ArgError("max_nbrs must be 1..64 for the device search");
+    if (h.has_overlay && (h.upper_R == 0 || h.upper_R > 64)) throw ArgError("overlay degree must be 1..64");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    auto up = [&](DevBuf &b, const void *src, size_t bytes) {
+      b.release();
+      b.reserve(std::max<size_t>(bytes, 4));
+      if (bytes)
+        hip_check(hipMemcpyAsync(b.ptr, src, bytes, hipMemcpyHostToDevice, ix->stream), "upload graph");
+    };
+    // rows of a HNSW adjacency list never repeat an id; scan once so the kernel can skip dedup.
+    bool dup = false;
+    for (uint64_t i = 0; i < h.n && !dup; ++i) {
+      const uint32_t *r = &h.l0[i * h.R];
+      for (uint32_t a = 0; a < h.R && r[a] != 0xffffffffu && !dup; ++a)
+        for (uint32_t b = 0; b < a; ++b)
+          if (r[a] == r[b]) {
+            dup = true;
+            break;
+          }
+    }
+    up(ix->l0, h.l0.data(), h.l0.size() * 4);
+    up(ix->levels, h.levels.data(), h.levels.size() * 4);
+    up(ix->upper_off, h.upper_off.data(), h.upper_off.size() * 8);
+    up(ix->upper_edges, h.upper_edges.data(), h.upper_edges.size() * 4);
+    up(ix->eps, h.eps.data(), h.eps.size() * 4);
+    hip_check(hipStreamSynchronize(ix->stream), "sync");
+    ix->R = h.R;
+    ix->upper_R = h.upper_R;
+    ix->ep = h.ep;
+    ix->n_eps = static_cast<uint32_t>(h.eps.size());
+    ix->has_overlay = h.has_overlay;
+    ix->dedup = dup;
+    ix->graph_n = h.n;
+    ix->has_graph = true;
+  });
+}
+
+int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uint64_t nq,
+                                    uint32_t k, uint32_t ef, uint32_t *d_ids, float *d_dists,
+                                    uint32_t *d_counters, void *stream) {
+  return guarded([&] {
+    if (!ix || (nq && (!d_queries || !d_ids))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    do_search(ix, d_queries, nq, k, ef, d_ids, d_dists, d_counters,
+              static_cast<hipStream_t>(stream));
+  });
+}
+
+int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
+                             uint32_t ef, uint32_t *ids, float *dists, uint32_t *counters) {
+  return guarded([&] {
+    if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (nq == 0 || k == 0) return;
+    ix->q_buf.reserve(nq * ix->dim * 4);
+    ix->id_buf.reserve(nq * k * 4);
+    ix->dist_buf.reserve(nq * k * 4);
+    ix->cnt_buf.reserve(nq * 16);
+    hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice,
+                             ix->stream), "upload queries");
+    do_search(ix, ix->q_buf.as<float>(), nq, k, ef, ix->id_buf.as<uint32_t>(),
+              ix->dist_buf.as<float>(), ix->cnt_buf.as<uint32_t>(), ix->stream);
+    hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    if (dists)
+      hip_check(hipMemcpyAsync(dists, ix->dist_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    if (counters)
+      hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipStreamSynchronize(ix->stream), "search");
+  });
+}
+
+int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, const uint32_t *ids,
+                          uint32_t n, float *out) {
+  return guarded([&] {
+    if (!ix || (nq && (!queries || !out)) || (n && !ids)) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (!ix->base.ptr) throw ArgError("index has no base vectors");
+    if (nq == 0 || n == 0) return;
+    if (nq > 65535) throw ArgError("at most 65535 queries per call");
+    for (uint32_t i = 0; i < n; ++i)
+      if (ids[i] >= ix->n) throw ArgError("id out of range");
+    ix->q_buf.reserve(nq * ix->dim * 4);
+    ix->dlist_buf.reserve(static_cast<size_t>(n) * 4);
+    ix->dout_buf.reserve(nq * n * 4);
+    hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
+    hip_check(hipMemcpyAsync(ix->dlist_buf.ptr, ids, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
+    SearchParams p = base_params(ix);
+    p.queries = ix->q_buf.as<float>();
+    p.q_stride = ix->dim;
+    hip_check(alaya_amd::launch_row_distances(p, ix->dlist_buf.as<uint32_t>(), n,
+                                              static_cast<uint32_t>(nq), ix->dout_buf.as<float>(),
+                                              ix->stream), "distance launch");
+    hip_check(hipMemcpyAsync(out, ix->dout_buf.ptr, nq * n * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipStreamSynchronize(ix->stream), "distances");
+  });
+}
+
+int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots) {
+  return guarded([&] {
+    if (!ix) throw ArgError("null index");
+    if (log2_slots != 0 && (log2_slots < 6 || log2_slots > 15)) throw ArgError("log2_slots must be 0 or 6..15");
+    ix->hash_log2_override = log2_slots;
+  });
+}
+
+int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,
+                     int *metric, uint64_t *device_bytes) {
+  return guarded([&] {
+    if (!ix) throw ArgError("null index");
+    if (n) *n = ix->n;
+    if (dim) *dim = ix->dim;
+    if (stride) *stride = ix->stride;
+    if (metric) *metric = ix->metric;
+    if (device_bytes) *device_bytes = ix->device_bytes();
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// Launch interface between the C-ABI layer (capi.cpp) and the device code (search_kernels.hip).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace alaya_amd {
+
+// Everything one search launch reads or writes.  All pointers are device pointers.
+struct SearchParams {
+  // base rows (RawSpace storage): n rows of `stride` floats, first `dim` used, zero padded
+  const float *base;
+  uint64_t n;
+  uint32_t dim;
+  uint32_t stride;        // multiple of 32 floats (128 B rows, 16 B aligned float4 loads)
+  const uint32_t *valid;  // SequentialStorage validity bitmap as 32-bit words; nullptr = all valid
+  bool ip;                // IP / COS (negated inner product) vs L2
+  // level-0 adjacency (Graph), n x R, -1 padded
+  const uint32_t *l0;
+  uint32_t R;
+  bool dedup_edges;       // some row repeats an id: drop later occurrences in-kernel
+  // overlay (OverlayGraph); levels == nullptr -> NSG-style entry points
+  const uint32_t *levels;
+  const uint64_t *upper_off;
+  const uint32_t *upper_edges;
+  uint32_t upper_R;
+  uint32_t ep;
+  const uint32_t *eps;
+  uint32_t n_eps;
+  // batch
+  const float *queries;   // nq rows of q_stride floats
+  uint64_t nq;
+  uint32_t q_stride;
+  uint32_t k;
+  uint32_t ef;
+  uint32_t *out_ids;      // nq x k
+  float *out_dists;       // nq x k (nullable)
+  uint32_t *out_counters; // nq x 4 (n_dist, n_expand, n_dist_upper, n_hops_upper), nullable
+  // scratch
+  uint32_t *work_counter; // zeroed before each launch
+  uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area
+  uint32_t hash_log2;     // LDS visited table = 1 << hash_log2 slots
+};
+
+size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2);
+hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu);
+hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream);
+// out[q * n + i] = dist(queries[q], base[ids[i]]) for q < nq (bit-exact device distance)
+hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint32_t n,
+                                uint32_t nq, float *out, hipStream_t stream);
+
+}  // namespace alaya_amd

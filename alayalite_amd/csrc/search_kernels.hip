@@ -1,0 +1,548 @@
+// MI355X (gfx950) device code for the HNSW best-first search hot path.
+//
+// One wavefront (64 lanes) owns one query at a time; workgroups are single waves that pull query
+// indices from a device work counter until the batch is drained (persistent blocks).  Per query:
+//   * query vector staged in LDS, zero-padded to the row stride;
+//   * the candidate pool (the reference's LinearPool, include/utils/query_utils.hpp:236-312) is a
+//     sorted LDS array of (dist, id|checked) with capacity ef;
+//   * the visited set (DynamicBitset, query_utils.hpp:69-115) is an exact LDS open-addressing hash
+//     table that spills to a per-slot global bitset when it fills;
+//   * one expansion = read a 128 B adjacency row, filter visited ids in adjacency order, compute all
+//     new distances at once (8 lanes per row, 8 rows per wave pass, 128 B-coalesced row chunks), then
+//     merge the batch into the pool with a wave-parallel stable merge that is provably identical to
+//     inserting the neighbours one by one (graph_search_job.hpp:237-251 + LinearPool::insert).
+// The distance reproduces l2_sqr_avx2 / ip_sqr_avx2 (include/simd/distance_l2.ipp:54-116,
+// distance_ip.ipp:56-111) bit for bit: lane m of a row group owns partial sums acc[4m..4m+3]
+// (element 32t+j -> acc[j]), the 8-lane combine follows the AVX2 horizontal tree exactly.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "search_kernels.h"
+
+namespace alaya_amd {
+
+namespace {
+
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr uint32_t kChecked = 0x80000000u;
+constexpr uint32_t kIdMask = 0x7fffffffu;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_sync() {
+  // One workgroup == one wave: the barrier orders LDS traffic between lanes at negligible cost.
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t v, uint32_t log2h) {
+  return (v * 0x9E3779B1u) >> (32 - log2h);
+}
+
+struct Lds {
+  float *q;          // stride floats
+  float *pd;         // ef + 1 pool distances
+  uint32_t *pi;      // ef + 1 pool ids (bit 31 = checked)
+  uint32_t *hash;    // 1 << hash_log2 visited slots
+  uint32_t *cid;     // 64 candidate ids (adjacency order)
+  float *cd;         // 64 candidate distances
+  float *sd;         // 64 sorted accepted distances
+};
+
+template <bool kIP>
+__device__ __forceinline__ void accumulate(const float4 x, const float4 y, float &a0, float &a1,
+                                           float &a2, float &a3) {
+  if (kIP) {  // acc = fma(x, y, acc)              (distance_ip.ipp:82-85)
+    a0 = fmaf(x.x, y.x, a0); a1 = fmaf(x.y, y.y, a1);
+    a2 = fmaf(x.z, y.z, a2); a3 = fmaf(x.w, y.w, a3);
+  } else {    // diff = x - y; acc = fma(diff, diff, acc)  (distance_l2.ipp:74-83)
+    const float d0 = x.x - y.x, d1 = x.y - y.y, d2 = x.z - y.z, d3 = x.w - y.w;
+    a0 = fmaf(d0, d0, a0); a1 = fmaf(d1, d1, a1);
+    a2 = fmaf(d2, d2, a2); a3 = fmaf(d3, d3, a3);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Distance of the query (LDS) to `n` rows listed in ids[0..n) -> out[0..n).  8 lanes per row.
+// --------------------------------------------------------------------------------------------
+template <bool kIP, int kChunks>
+__device__ __forceinline__ void row_distances(const SearchParams &p, const float *q,
+                                              const uint32_t *ids, int n, float *out) {
+  const int lane = lane_id();
+  const int g = lane >> 3, m = lane & 7;
+  const int T = kChunks > 0 ? kChunks : static_cast<int>(p.dim >> 5);
+  const int rem = static_cast<int>(p.dim) - 32 * T;
+  const int nb8 = rem >> 3;
+  const int tail_begin = 32 * T + 8 * nb8;
+  for (int base = 0; base < n; base += 8) {
+    const int r = base + g;
+    const bool act = r < n;
+    const uint32_t id = act ? ids[r] : 0u;
+    const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (act) {
+      const float4 *rp = reinterpret_cast<const float4 *>(row) + m;
+      const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+      if constexpr (kChunks > 0) {
+#pragma unroll
+        for (int t = 0; t < kChunks; ++t) {
+          const float4 y = rp[8 * t];
+          const float4 x = qp[8 * t];
+          accumulate<kIP>(x, y, a0, a1, a2, a3);
+        }
+      } else {
+#pragma unroll 6
+        for (int t = 0; t < T; ++t) {
+          const float4 y = rp[8 * t];
+          const float4 x = qp[8 * t];
+          accumulate<kIP>(x, y, a0, a1, a2, a3);
+        }
+      }
+      // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1); rows are 16 B aligned.
+      if (m < 2) {
+        for (int b = 0; b < nb8; ++b) {
+          const int e = 32 * T + 8 * b + 4 * m;
+          const float4 y = *reinterpret_cast<const float4 *>(row + e);
+          const float4 x = *reinterpret_cast<const float4 *>(q + e);
+          accumulate<kIP>(x, y, a0, a1, a2, a3);
+        }
+      }
+    }
+    // (acc0+acc1) + (acc2+acc3) per lane of the 8-wide vector: lanes m^2 then m^4.
+    a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
+    a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+    // lane m==0 holds v[0..3], lane m==1 holds v[4..7]: s[j] = v[j] + v[j+4].
+    const float s0 = a0 + __shfl_xor(a0, 1), s1 = a1 + __shfl_xor(a1, 1);
+    const float s2 = a2 + __shfl_xor(a2, 1), s3 = a3 + __shfl_xor(a3, 1);
+    if (act && m == 0) {
+      float res = (s0 + s1) + (s2 + s3);
+      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e) {
+        if (kIP) {
+          res = fmaf(q[e], row[e], res);
+        } else {
+          const float d = q[e] - row[e];
+          res = fmaf(d, d, res);
+        }
+      }
+      if (kIP) res = -res;
+      if (p.valid != nullptr && !((p.valid[id >> 5] >> (id & 31)) & 1u)) res = FLT_MAX;
+      out[r] = res;
+    }
+  }
+  wave_sync();
+}
+
+// --------------------------------------------------------------------------------------------
+// Visited set: exact.  Returns true if v was not yet in the set (and inserts it).
+// --------------------------------------------------------------------------------------------
+struct Visited {
+  uint32_t *tab;
+  uint32_t log2h;
+  uint32_t count;        // wave-uniform number of entries in the LDS table
+  uint32_t limit;        // switch to the global bitset above this many entries
+  bool spilled;          // wave-uniform
+  uint32_t *bits;        // per-slot global bitset (valid when spilled)
+};
+
+__device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
+  const uint32_t mask = (1u << vs.log2h) - 1u;
+  uint32_t h = hash_slot(v, vs.log2h);
+  for (;;) {
+    const uint32_t e = vs.tab[h];
+    if (e == v) return true;
+    if (e == kEmpty) return false;
+    h = (h + 1) & mask;
+  }
+}
+
+// All lanes with `act` insert their v; duplicates among lanes must have been removed.
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
+  bool fresh = false;
+  if (!vs.spilled) {
+    if (act) {
+      const uint32_t mask = (1u << vs.log2h) - 1u;
+      uint32_t h = hash_slot(v, vs.log2h);
+      for (;;) {
+        const uint32_t old = atomicCAS(&vs.tab[h], kEmpty, v);
+        if (old == kEmpty) { fresh = true; break; }
+        if (old == v) break;
+        h = (h + 1) & mask;
+      }
+    }
+    vs.count += __popcll(ballot(fresh));
+  } else if (act) {
+    if (!table_lookup(vs, v)) {
+      const uint32_t bit = 1u << (v & 31);
+      const uint32_t old = atomicOr(&vs.bits[v >> 5], bit);
+      fresh = (old & bit) == 0u;
+    }
+  }
+  return fresh;
+}
+
+__device__ void spill_begin(Visited &vs, uint64_t n_words) {
+  // zero this slot's global bitset once, then keep the LDS table as a read-only first level.
+  const int lane = lane_id();
+  for (uint64_t w = lane; w < n_words; w += 64) vs.bits[w] = 0u;
+  __threadfence_block();
+  wave_sync();
+  vs.spilled = true;
+}
+
+// --------------------------------------------------------------------------------------------
+// Pool (LinearPool).  size/cur are wave-uniform.  Checked flag lives in bit 31 of the id.
+// --------------------------------------------------------------------------------------------
+struct PoolState {
+  uint32_t size;
+  uint32_t cur;
+  uint32_t ef;
+};
+
+// number of pool entries with dist <= d (find_bsearch, strict '>' keeps equal ones first)
+__device__ __forceinline__ uint32_t pool_upper_bound(const float *pd, uint32_t size, float d) {
+  uint32_t lo = 0, hi = size;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pd[mid] > d) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+// number of sorted batch distances strictly below d
+__device__ __forceinline__ uint32_t batch_lower_bound(const float *sd, uint32_t n, float d) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sd[mid] < d) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Merge candidates held by lanes 0..nb-1 (arrival order = lane order, nb <= 64) into the pool.
+// Equivalent to calling LinearPool::insert(id_i, d_i) for i = 0..nb-1 in order.
+__device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d) {
+  const int lane = lane_id();
+  const bool full = ps.size == ps.ef;
+  const float last = full ? L.pd[ps.size - 1] : 0.f;
+  const bool acc = has && !(full && d >= last);
+  const uint64_t amask = ballot(acc);
+  const uint32_t n_acc = __popcll(amask);
+  if (n_acc == 0) return;
+  // stable rank of this candidate among accepted ones, ordered by (dist, arrival)
+  uint32_t rank = 0;
+  uint64_t rest = amask;
+  while (rest) {
+    const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
+    rest &= rest - 1;
+    const float dj = __shfl(d, j);
+    rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
+  }
+  if (acc) L.sd[rank] = d;
+  uint32_t pos = 0;
+  if (acc) pos = pool_upper_bound(L.pd, ps.size, d) + rank;
+  // first insertion position = position of the rank-0 element
+  const uint32_t first_pos = __shfl(pos, __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1);
+  wave_sync();
+  // shift pool entries [first_pos, size) up by #accepted strictly smaller, top chunk first.
+  for (int hi = static_cast<int>(ps.size); hi > static_cast<int>(first_pos); hi -= 64) {
+    const int j = hi - 64 + lane;
+    const bool mv = j >= static_cast<int>(first_pos);
+    float pdj = 0.f;
+    uint32_t pij = 0;
+    uint32_t dest = 0;
+    if (mv) {
+      pdj = L.pd[j];
+      pij = L.pi[j];
+      dest = static_cast<uint32_t>(j) + batch_lower_bound(L.sd, n_acc, pdj);
+    }
+    wave_sync();
+    if (mv && dest < ps.ef) {
+      L.pd[dest] = pdj;
+      L.pi[dest] = pij;
+    }
+    wave_sync();
+  }
+  if (acc && pos < ps.ef) {
+    L.pd[pos] = d;
+    L.pi[pos] = id;
+  }
+  wave_sync();
+  ps.size = min(ps.size + n_acc, ps.ef);
+  if (first_pos < ps.cur) ps.cur = first_pos;
+}
+
+// LinearPool::pop: mark cur checked, advance to the next unchecked entry.
+__device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L) {
+  const int lane = lane_id();
+  const uint32_t raw = L.pi[ps.cur];
+  wave_sync();
+  if (lane == 0) L.pi[ps.cur] = raw | kChecked;
+  uint32_t next = ps.size;
+  for (uint32_t b = ps.cur + 1; b < ps.size; b += 64) {
+    const uint32_t j = b + lane;
+    const bool un = j < ps.size && !(L.pi[j] & kChecked);
+    const uint64_t mk = ballot(un);
+    if (mk) {
+      next = b + __ffsll(static_cast<unsigned long long>(mk)) - 1;
+      break;
+    }
+  }
+  wave_sync();
+  ps.cur = next;
+  return raw & kIdMask;
+}
+
+// --------------------------------------------------------------------------------------------
+// The search kernel.
+// --------------------------------------------------------------------------------------------
+template <bool kIP, int kChunks>
+__global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  Lds L;
+  {
+    unsigned char *ptr = smem;
+    L.q = reinterpret_cast<float *>(ptr);
+    ptr += static_cast<size_t>(p.stride) * 4;
+    L.cid = reinterpret_cast<uint32_t *>(ptr);
+    ptr += 64 * 4;
+    L.cd = reinterpret_cast<float *>(ptr);
+    ptr += 64 * 4;
+    L.sd = reinterpret_cast<float *>(ptr);
+    ptr += 64 * 4;
+    L.pd = reinterpret_cast<float *>(ptr);
+    ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
+    L.pi = reinterpret_cast<uint32_t *>(ptr);
+    ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
+    L.hash = reinterpret_cast<uint32_t *>(ptr);
+  }
+  const uint32_t hsize = 1u << p.hash_log2;
+  const uint64_t bit_words = (p.n + 31) / 32;
+  uint32_t *slot_bits = p.overflow_bits + static_cast<uint64_t>(blockIdx.x) * bit_words;
+
+  for (;;) {
+    uint32_t qi = 0;
+    if (lane == 0) qi = atomicAdd(p.work_counter, 1u);
+    qi = __shfl(qi, 0);
+    if (qi >= p.nq) break;
+
+    // ---- per-query init ------------------------------------------------------------------
+    const float *qsrc = p.queries + static_cast<uint64_t>(qi) * p.q_stride;
+    for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
+    for (uint32_t e = lane; e < hsize; e += 64) L.hash[e] = kEmpty;
+    for (uint32_t e = lane; e <= p.ef; e += 64) {
+      L.pd[e] = 0.f;
+      L.pi[e] = 0u;
+    }
+    wave_sync();
+    Visited vs{L.hash, p.hash_log2, 0u, hsize / 2, false, slot_bits};
+    PoolState ps{0u, 0u, p.ef};
+    uint32_t n_dist = 0, n_expand = 0, n_dist_up = 0, n_hops_up = 0;
+
+    // ---- Graph::initialize_search (graph.hpp:148-158) ---------------------------------------
+    if (p.levels != nullptr) {
+      // OverlayGraph::initialize (overlay_graph.hpp:122-144): greedy descent, strict '<'.
+      uint32_t u = p.ep;
+      if (lane == 0) L.cid[0] = u;
+      wave_sync();
+      row_distances<kIP, kChunks>(p, L.q, L.cid, 1, L.cd);
+      float cur = L.cd[0];
+      ++n_dist_up;
+      for (int level = static_cast<int>(p.levels[u]); level > 0; --level) {
+        bool changed = true;
+        while (changed) {
+          changed = false;
+          const uint32_t *list = p.upper_edges + p.upper_off[u] +
+                                 static_cast<uint64_t>(level - 1) * p.upper_R;
+          const uint32_t v = lane < static_cast<int>(p.upper_R) ? list[lane] : kEmpty;
+          const uint64_t endm = ballot(lane < static_cast<int>(p.upper_R) && v == kEmpty);
+          const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1
+                               : static_cast<int>(p.upper_R);
+          ++n_hops_up;
+          wave_sync();
+          if (lane < cnt) L.cid[lane] = v;
+          wave_sync();
+          row_distances<kIP, kChunks>(p, L.q, L.cid, cnt, L.cd);
+          n_dist_up += cnt;
+          // first index of the minimum == the sequential strict-'<' scan's final choice
+          float dl = lane < cnt ? L.cd[lane] : FLT_MAX;
+          bool has = lane < cnt;
+          float mn = has ? dl : FLT_MAX;
+          for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+          const uint64_t at = ballot(has && dl == mn);
+          if (at && mn < cur) {
+            const int w = __ffsll(static_cast<unsigned long long>(at)) - 1;
+            u = __shfl(v, w);
+            cur = mn;
+            changed = true;
+          }
+          wave_sync();
+        }
+      }
+      // pool.insert(u, cur); vis.set(u)
+      if (lane == 0) {
+        L.pd[0] = cur;
+        L.pi[0] = u;
+      }
+      ps.size = 1;
+      ps.cur = 0;
+      visit(vs, u, lane == 0);
+      wave_sync();
+    } else {
+      // NSG-style entry points: insert each ep, then mark it visited (graph.hpp:153-156)
+      for (uint32_t b = 0; b < p.n_eps; b += 64) {
+        const uint32_t cnt = min(64u, p.n_eps - b);
+        const bool has = static_cast<uint32_t>(lane) < cnt;
+        uint32_t v = has ? p.eps[b + lane] : 0u;
+        if (has) L.cid[lane] = v;
+        wave_sync();
+        for (uint32_t c = 0; c < cnt; c += 8) {
+          row_distances<kIP, kChunks>(p, L.q, L.cid + c, min(8u, cnt - c), L.cd + c);
+        }
+        n_dist_up += cnt;
+        const float d = has ? L.cd[lane] : 0.f;
+        wave_sync();
+        pool_merge(ps, L, has, v, d);
+        // duplicates among eps are all inserted (no visited check in the reference loop)
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint32_t vj = __shfl(v, j);
+          if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
+          visit(vs, vj, lane == 0);
+        }
+        wave_sync();
+      }
+    }
+
+    // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
+    while (ps.cur < ps.size) {
+      const uint32_t u = pool_pop(ps, L);
+      ++n_expand;
+      const uint32_t *adj = p.l0 + static_cast<uint64_t>(u) * p.R;
+      uint32_t v = lane < static_cast<int>(p.R) ? adj[lane] : kEmpty;
+      const uint64_t endm = ballot(lane < static_cast<int>(p.R) && v == kEmpty);
+      const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1 : static_cast<int>(p.R);
+      bool act = lane < cnt;
+      if (p.dedup_edges) {  // graphs with repeated ids in a row: keep the first occurrence only
+        for (int j = 0; j < cnt; ++j) {
+          const uint32_t vj = __shfl(v, j);
+          if (j < lane && vj == v) act = false;
+        }
+      }
+      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
+      const bool fresh = visit(vs, v, act);
+      const uint64_t fm = ballot(fresh);
+      const int nf = __popcll(fm);
+      if (nf == 0) continue;
+      // compact fresh ids in adjacency order
+      const uint32_t slot = __popcll(fm & ((1ull << lane) - 1ull));
+      if (fresh) L.cid[slot] = v;
+      wave_sync();
+      row_distances<kIP, kChunks>(p, L.q, L.cid, nf, L.cd);
+      n_dist += nf;
+      const bool has = lane < nf;
+      const uint32_t cid = has ? L.cid[lane] : 0u;
+      const float cd = has ? L.cd[lane] : 0.f;
+      wave_sync();
+      pool_merge(ps, L, has, cid, cd);
+    }
+
+    // ---- results (ids[i] = pool.id(i), distances[i] = pool.dist(i)) --------------------------
+    for (uint32_t i = lane; i < p.k; i += 64) {
+      uint32_t id = 0;
+      float d = 0.f;
+      if (i < ps.size) {
+        id = L.pi[i] & kIdMask;
+        d = L.pd[i];
+      }
+      p.out_ids[static_cast<uint64_t>(qi) * p.k + i] = id;
+      if (p.out_dists) p.out_dists[static_cast<uint64_t>(qi) * p.k + i] = d;
+    }
+    if (p.out_counters && lane == 0) {
+      uint32_t *c = p.out_counters + static_cast<uint64_t>(qi) * 4;
+      c[0] = n_dist;
+      c[1] = n_expand;
+      c[2] = n_dist_up;
+      c[3] = n_hops_up;
+    }
+    wave_sync();
+  }
+}
+
+// Plain batched distance kernel (one query, list of ids) -- used by the rerank and by tests.
+template <bool kIP>
+__global__ void __launch_bounds__(64) row_distance_kernel(SearchParams p, const uint32_t *ids,
+                                                          uint32_t n, float *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float *q = reinterpret_cast<float *>(smem);
+  uint32_t *lid = reinterpret_cast<uint32_t *>(smem + static_cast<size_t>(p.stride) * 4);
+  float *ld = reinterpret_cast<float *>(lid + 64);
+  const int lane = lane_id();
+  const float *qsrc = p.queries + static_cast<uint64_t>(blockIdx.y) * p.q_stride;
+  for (uint32_t e = lane; e < p.stride; e += 64) q[e] = e < p.dim ? qsrc[e] : 0.f;
+  wave_sync();
+  for (uint32_t b = blockIdx.x * 64; b < n; b += gridDim.x * 64) {
+    const uint32_t cnt = min(64u, n - b);
+    if (static_cast<uint32_t>(lane) < cnt) lid[lane] = ids[b + lane];
+    wave_sync();
+    for (uint32_t c = 0; c < cnt; c += 8)
+      row_distances<kIP, 0>(p, q, lid + c, min(8u, cnt - c), ld + c);
+    if (static_cast<uint32_t>(lane) < cnt)
+      out[static_cast<uint64_t>(blockIdx.y) * n + b + lane] = ld[lane];
+    wave_sync();
+  }
+}
+
+}  // namespace
+
+size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2) {
+  return static_cast<size_t>(stride) * 4 + 3 * 64 * 4 + 2 * (((ef + 1) * 4 + 15) / 16 * 16) +
+         (static_cast<size_t>(1) << hash_log2) * 4;
+}
+
+template <bool kIP, int kChunks>
+static const void *kernel_ptr() {
+  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks>);
+}
+
+const void *search_kernel_symbol(bool ip, uint32_t dim) {
+  const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
+#define ALAYA_CASE(C)                                                        \
+  if (chunks == C) return ip ? kernel_ptr<true, C>() : kernel_ptr<false, C>();
+  ALAYA_CASE(4)
+  ALAYA_CASE(8)
+  ALAYA_CASE(16)
+  ALAYA_CASE(24)
+  ALAYA_CASE(30)
+  ALAYA_CASE(32)
+#undef ALAYA_CASE
+  return ip ? kernel_ptr<true, 0>() : kernel_ptr<false, 0>();
+}
+
+hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream) {
+  const void *fn = search_kernel_symbol(p.ip, p.dim);
+  SearchParams arg = p;
+  void *args[] = {&arg};
+  return hipLaunchKernel(fn, dim3(grid), dim3(64), args, lds, stream);
+}
+
+hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint32_t n,
+                                uint32_t nq, float *out, hipStream_t stream) {
+  const size_t lds = static_cast<size_t>(p.stride) * 4 + 128 * 4;
+  const int gx = static_cast<int>(std::min<uint32_t>((n + 63) / 64, 1024u));
+  if (p.ip) {
+    hipLaunchKernelGGL(row_distance_kernel<true>, dim3(gx, nq), dim3(64), lds, stream, p, ids, n, out);
+  } else {
+    hipLaunchKernelGGL(row_distance_kernel<false>, dim3(gx, nq), dim3(64), lds, stream, p, ids, n, out);
+  }
+  return hipGetLastError();
+}
+
+hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu) {
+  const void *fn = search_kernel_symbol(p.ip, p.dim);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, lds);
+}
+
+}  // namespace alaya_amd

@@ -1,0 +1,102 @@
+/*
+ * alaya_hip.h -- C ABI of the MI355X search engine (libalaya_hip.so).
+ *
+ * This is the drop-in boundary for AlayaLite's search hot path.  Plain pointers and sizes only;
+ * every call returns an int status (ALAYA_OK == 0) and alaya_last_error() gives the message of
+ * the last failure on the calling thread.  Host buffers are copied; *_device variants take device
+ * pointers and a hipStream_t (passed as void*) and are asynchronous on that stream.
+ *
+ * Reference interfaces each group replaces (paths relative to the AlayaLite repo root):
+ *   alaya_index_*            PyIndex<HNSWBuilder<RawSpace>, Space> state and lifetime
+ *                            (python/include/index.hpp:85-506, PyIndexInterface :508-587)
+ *   alaya_index_set_base     RawSpace ctor/fit + SequentialStorage (include/space/raw_space.hpp:81-140,
+ *                            include/storage/sequential_storage.hpp:53-84) -- rows moved to HBM
+ *   alaya_index_set_graph    Graph + OverlayGraph (include/index/graph/graph.hpp:44-158,
+ *                            overlay_graph.hpp:26-144) -- adjacency moved to HBM
+ *   alaya_index_batch_search PyIndex::batch_search / batch_search_with_distance
+ *                            (python/include/index.hpp:289-451) -> GraphSearchJob::search
+ *                            (include/executor/jobs/graph_search_job.hpp:221-299) on the device
+ *   alaya_index_search       PyIndex::search (index.hpp:236-258) -> search_solo (:302-371)
+ *   alaya_index_distances    RawSpace::QueryComputer::operator() (raw_space.hpp:297-304) over
+ *                            simd::l2_sqr / ip_sqr (include/simd/distance_l2.ipp:729-742,
+ *                            distance_ip.ipp:739-751) -- the metric plugin surface
+ *                            (include/space/space_concepts.hpp:31-73)
+ *   alaya_graph_*            HNSWBuilder::build_graph (include/index/graph/hnsw/hnsw_builder.hpp:98-194)
+ *                            and Graph::save/load (graph.hpp:165-238)
+ */
+#ifndef ALAYA_HIP_H_
+#define ALAYA_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALAYA_OK 0
+#define ALAYA_ERR_ARG 1      /* invalid argument (Python: ValueError)            */
+#define ALAYA_ERR_RUNTIME 2  /* runtime failure (Python: RuntimeError)           */
+#define ALAYA_ERR_DEVICE 3   /* HIP error / no device (Python: RuntimeError)     */
+
+/* MetricType values of include/utils/metric_type.hpp */
+#define ALAYA_METRIC_L2 0
+#define ALAYA_METRIC_IP 1
+#define ALAYA_METRIC_COS 2
+
+typedef struct alaya_index alaya_index;
+typedef struct alaya_graph alaya_graph;
+
+const char *alaya_last_error(void);
+/* Number of visible HIP devices (0 when none). */
+int alaya_device_count(int *count);
+
+/* ---- host graph (builder + reference on-disk format) --------------------------------------- */
+/* data: n x dim float32 row-major (normalised already for COS).  seed 100 = reference default. */
+int alaya_graph_build_hnsw(const float *data, uint64_t n, uint32_t dim, int metric, uint32_t R,
+                           uint32_t ef_construction, uint32_t num_threads, uint64_t seed,
+                           alaya_graph **out);
+int alaya_graph_load(const char *path, int id_bytes, alaya_graph **out);
+int alaya_graph_save(const alaya_graph *g, const char *path, int id_bytes, uint64_t capacity);
+/* sizes: n, R, has_overlay, upper_R, ep, max_level, n_upper_edges, n_eps */
+int alaya_graph_info(const alaya_graph *g, uint64_t *n, uint32_t *R, int *has_overlay,
+                     uint32_t *upper_R, uint32_t *ep, uint32_t *max_level,
+                     uint64_t *n_upper_edges, uint32_t *n_eps);
+/* copy out: l0[n*R], levels[n], upper_off[n], upper_edges[n_upper_edges], eps[n_eps]; any NULL skipped */
+int alaya_graph_export(const alaya_graph *g, uint32_t *l0, uint32_t *levels, uint64_t *upper_off,
+                       uint32_t *upper_edges, uint32_t *eps);
+/* build a graph object from host arrays (levels == NULL -> NSG-style eps) */
+int alaya_graph_import(uint64_t n, uint32_t R, const uint32_t *l0, const uint32_t *levels,
+                       const uint64_t *upper_off, const uint32_t *upper_edges,
+                       uint64_t n_upper_edges, uint32_t upper_R, uint32_t ep, const uint32_t *eps,
+                       uint32_t n_eps, alaya_graph **out);
+void alaya_graph_free(alaya_graph *g);
+
+/* ---- device index ---------------------------------------------------------------------------- */
+int alaya_index_create(int device, alaya_index **out);
+void alaya_index_destroy(alaya_index *ix);
+/* rows: n x dim float32 host array (row pitch dim).  valid_bitmap: ceil(n/8) bytes in the
+ * SequentialStorage layout (bit i%8 of byte i/8 set = valid) or NULL for all valid. */
+int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_t dim, int metric,
+                         const uint8_t *valid_bitmap);
+int alaya_index_set_graph(alaya_index *ix, const alaya_graph *g);
+/* Batched search on host buffers.  ids: nq x k; dists (nullable): nq x k; counters (nullable):
+ * nq x 4 uint32 = (n_dist, n_expand, n_dist_upper, n_hops_upper). */
+int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
+                             uint32_t ef, uint32_t *ids, float *dists, uint32_t *counters);
+/* Same on device buffers, asynchronous on `stream` (hipStream_t; NULL = default stream). */
+int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uint64_t nq,
+                                    uint32_t k, uint32_t ef, uint32_t *d_ids, float *d_dists,
+                                    uint32_t *d_counters, void *stream);
+/* out[q*n + i] = metric distance(queries[q], row ids[i]), bit-exact with the search kernel. */
+int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, const uint32_t *ids,
+                          uint32_t n, float *out);
+/* Tuning / introspection: LDS visited-table size (log2 slots; 0 = automatic). */
+int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots);
+int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,
+                     int *metric, uint64_t *device_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALAYA_HIP_H_ */

@@ -1,0 +1,232 @@
+"""Device parity: the HIP path (through the C ABI) against the CPU restatement, bit for bit.
+
+Bar: integer/index outputs (neighbour ids, counters) identical; float distances identical in
+their bit pattern (the device reproduces the reference's AVX2 reduction order exactly)."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph_view(native, orc, base, metric=0, threads=1, R=32, valid=None):
+    g = native.Graph.build(base, metric, R, 100, threads, 100)
+    l0, levels, off, ue, ep, upper_r, _ = g.arrays()
+    view = orc.IndexView(base, l0, levels, off, ue, upper_r, ep, metric=metric, valid=valid)
+    return g, view
+
+
+def _dev(native, base, g, metric=0, valid=None):
+    d = native.DeviceIndex(0)
+    d.set_base(base, metric, valid)
+    d.set_graph(g)
+    return d
+
+
+def _check(view, dev, queries, k, ef):
+    ids, dists, cnt = dev.search(queries, k, ef)
+    for i, q in enumerate(queries):
+        r_ids, r_d, r_c = view.search(q, k, ef, with_counters=True)
+        assert np.array_equal(ids[i], r_ids), (i, ids[i], r_ids)
+        assert np.array_equal(dists[i].view(np.uint32), r_d.view(np.uint32)), (i, dists[i], r_d)
+        assert tuple(cnt[i]) == tuple(r_c), (i, cnt[i], r_c)
+    return ids
+
+
+@pytest.mark.parametrize("dim", [1, 2, 5, 8, 13, 16, 24, 31, 32, 33, 40, 64, 96, 100, 127, 128, 129,
+                                 200, 255, 256, 384, 512, 768, 800, 960, 1000, 1024])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_distance_kernel_bit_exact(native, orc, dim, metric):
+    rng = np.random.default_rng(dim * 7 + metric)
+    base = rng.uniform(-1, 1, (300, dim)).astype(np.float32)
+    q = rng.uniform(-1, 1, (3, dim)).astype(np.float32)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, metric)
+    ids = rng.permutation(300).astype(np.uint32)[:137]
+    out = dev.distances(q, ids)
+    for a in range(3):
+        ref = np.array([orc.dist(metric, q[a], base[i]) for i in ids], np.float32)
+        assert np.array_equal(out[a].view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("ef", [10, 20, 50, 100, 200])
+def test_search_c1_bit_exact(native, orc, c1, ef):
+    base, queries = c1
+    g, view = _graph_view(native, orc, base)
+    _check(view, _dev(native, base, g), queries, 10, ef)
+
+
+@pytest.mark.parametrize("k,ef", [(1, 1), (1, 10), (10, 10), (3, 3), (16, 16), (100, 100), (64, 300)])
+def test_search_k_ef_shapes(native, orc, c1, k, ef):
+    base, queries = c1
+    g, view = _graph_view(native, orc, base)
+    _check(view, _dev(native, base, g), queries, k, ef)
+
+
+def test_k_larger_than_ef(native, orc, c1):
+    """k > ef reads past LinearPool's live entries in the reference (slot ef holds the last dropped
+    neighbour, beyond it is out of bounds: query_utils.hpp:238, graph_search_job.hpp:254-256).
+    The engine defines it: the first ef entries are the pool, the rest are (id 0, dist 0.0)."""
+    base, queries = c1
+    g, view = _graph_view(native, orc, base)
+    ids, dists, _ = _dev(native, base, g).search(queries, 8, 5)
+    for i, q in enumerate(queries):
+        r_ids, r_d = view.search(q, 5, 5)
+        assert np.array_equal(ids[i, :5], r_ids) and np.array_equal(dists[i, :5], r_d)
+        assert not ids[i, 5:].any() and not dists[i, 5:].any()
+
+
+@pytest.mark.parametrize("log2", [6, 8, 11])
+def test_visited_spill_path(native, orc, c1, log2):
+    """Tiny LDS tables force the per-slot global bitset; results must not change."""
+    base, queries = c1
+    g, view = _graph_view(native, orc, base)
+    dev = _dev(native, base, g)
+    dev.set_hash_log2(log2)
+    _check(view, dev, queries, 10, 100)
+
+
+@pytest.mark.parametrize("metric", [1, 2])
+def test_search_ip_cos(native, orc, metric):
+    rng = np.random.default_rng(3 + metric)
+    base = rng.standard_normal((2000, 96)).astype(np.float32)
+    queries = rng.standard_normal((20, 96)).astype(np.float32)
+    if metric == 2:
+        base = np.stack([orc.normalize(r) for r in base])
+        queries = np.stack([orc.normalize(r) for r in queries])
+    g, view = _graph_view(native, orc, base, metric=metric)
+    _check(view, _dev(native, base, g, metric), queries, 10, 64)
+
+
+def test_search_gist_shaped(native, orc):
+    rng = np.random.default_rng(9)
+    centres = rng.uniform(0, 0.5, (16, 960)).astype(np.float32)
+    base = np.clip(centres[rng.integers(0, 16, 6000)] + rng.normal(0, 0.05, (6000, 960)), 0, 1).astype(np.float32)
+    queries = np.clip(centres[rng.integers(0, 16, 24)] + rng.normal(0, 0.05, (24, 960)), 0, 1).astype(np.float32)
+    g, view = _graph_view(native, orc, base, threads=8)
+    _check(view, _dev(native, base, g), queries, 10, 80)
+
+
+def test_search_sift_shaped_many_queries(native, orc):
+    rng = np.random.default_rng(4)
+    base = rng.integers(0, 128, (20000, 128)).astype(np.float32)
+    queries = rng.integers(0, 128, (3000, 128)).astype(np.float32)
+    g, view = _graph_view(native, orc, base, threads=8)
+    dev = _dev(native, base, g)
+    ids, dists, cnt = dev.search(queries, 10, 40)
+    sample = rng.choice(3000, 60, replace=False)
+    for i in sample:
+        r_ids, r_d = view.search(queries[i], 10, 40)
+        assert np.array_equal(ids[i], r_ids) and np.array_equal(dists[i].view(np.uint32), r_d.view(np.uint32))
+
+
+def test_invalid_rows_get_flt_max(native, orc, c1):
+    """RawSpace::QueryComputer returns FLT_MAX for rows cleared in the validity bitmap
+    (raw_space.hpp:298-300)."""
+    base, queries = c1
+    valid = np.full(1000 // 8, 0xFF, np.uint8)
+    valid[3] = 0x5A
+    valid[50] = 0x00
+    g, view = _graph_view(native, orc, base, valid=valid)
+    _check(view, _dev(native, base, g, valid=valid), queries, 10, 100)
+
+
+def test_nsg_style_entry_points(native, orc, c1):
+    base, queries = c1
+    g0 = native.Graph.build(base, 0, 32, 100, 1, 100)
+    l0 = g0.arrays()[0]
+    eps = np.array([5, 77, 5, 901], np.uint32)  # repeated ep inserted twice, like the reference loop
+    g = native.Graph.from_arrays(l0, None, None, None, 0, 0, eps)
+    dev = _dev(native, base, g)
+    ids, dists, cnt = dev.search(queries, 10, 50)
+    for i, q in enumerate(queries):
+        r_ids, r_d = _nsg_model(orc, base, l0, eps, q, 10, 50)
+        assert np.array_equal(ids[i], r_ids) and np.array_equal(dists[i].view(np.uint32), r_d.view(np.uint32))
+
+
+def _nsg_model(orc, base, l0, eps, q, k, ef):
+    """Pure-Python restatement of search_solo with Graph::initialize_search's eps branch
+    (graph.hpp:153-156), driving the oracle's LinearPool and distance."""
+    pool = orc.Pool(base.shape[0], ef)
+    vis = set()
+    for e in eps:
+        pool.insert(int(e), float(orc.l2(q, base[e])))
+        vis.add(int(e))
+    while pool.has_next():
+        u = pool.pop()
+        for v in l0[u]:
+            if v == 0xFFFFFFFF:
+                break
+            if int(v) in vis:
+                continue
+            vis.add(int(v))
+            pool.insert(int(v), float(orc.l2(q, base[v])))
+    ids = np.array([pool.id(i) for i in range(k)], np.uint32)
+    d = np.array([pool.dist(i) for i in range(k)], np.float32)
+    return ids, d
+
+
+def test_duplicate_edges_dedup(native, orc, c1):
+    base, queries = c1
+    g0 = native.Graph.build(base, 0, 32, 100, 1, 100)
+    l0, levels, off, ue, ep, upper_r, _ = g0.arrays()
+    l0 = l0.copy()
+    for u in range(0, 1000, 3):  # repeat an earlier neighbour inside the row
+        cnt = int((l0[u] != 0xFFFFFFFF).sum())
+        if 2 <= cnt < 32:
+            l0[u, cnt] = l0[u, 0]
+    g = native.Graph.from_arrays(l0, levels, off, ue, upper_r, ep)
+    view = orc.IndexView(base, l0, levels, off, ue, upper_r, ep)
+    _check(view, _dev(native, base, g), queries, 10, 50)
+
+
+def test_index_api_end_to_end(native, orc, c1):
+    import alayalite_amd
+
+    base, queries = c1
+    client = alayalite_amd.Client()
+    index = client.create_index("c1", capacity=1000)
+    index.fit(base, ef_construction=100, num_threads=1)
+    ids = index.batch_search(queries, 10, 100)
+    ids2, dists = index.batch_search_with_distance(queries, 10, 100)
+    one = index.search(queries[0], 10, 100)
+    assert ids.dtype == np.uint32 and ids.shape == (10, 10)
+    assert np.array_equal(ids, ids2) and np.array_equal(one, ids[0])
+    l0, levels, off, ue, ep, upper_r, _ = index.native().graph_arrays()
+    view = orc.IndexView(base, l0, levels, off, ue, upper_r, ep)
+    for i, q in enumerate(queries):
+        r_ids, r_d = view.search(q, 10, 100)
+        assert np.array_equal(ids[i], r_ids) and np.array_equal(dists[i].view(np.uint32), r_d.view(np.uint32))
+    from alayalite_amd.utils import calc_gt, calc_recall
+
+    assert calc_recall(ids, calc_gt(base, queries, 10)) >= 0.9
+    assert np.array_equal(index.get_data_by_id(7), base[7])
+
+
+def test_index_save_load(native, c1, tmp_path):
+    import alayalite_amd
+
+    base, queries = c1
+    client = alayalite_amd.Client(str(tmp_path))
+    index = client.create_index("saved", capacity=2000)
+    index.fit(base)
+    before = index.batch_search(queries, 10, 50)
+    client.save_index("saved")
+    again = alayalite_amd.Client(str(tmp_path)).get_index("saved")
+    assert np.array_equal(again.batch_search(queries, 10, 50), before)
+    assert again.get_dim() == 128
+
+
+def test_uint64_ids_and_int_dtype(native, c1):
+    import alayalite_amd
+
+    rng = np.random.default_rng(1)
+    base = rng.integers(0, 50, (1000, 64)).astype(np.int32)
+    queries = rng.integers(0, 50, (5, 64)).astype(np.int32)
+    index = alayalite_amd.Client().create_index("u64", capacity=1000, id_type=np.uint64, data_type=np.int32)
+    index.fit(base)
+    ids = index.batch_search(queries, 10, 100)
+    assert ids.dtype == np.uint64
+    from alayalite_amd.utils import calc_gt, calc_recall
+
+    assert calc_recall(ids, calc_gt(base, queries, 10)) >= 0.9
