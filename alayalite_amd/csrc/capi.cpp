@@ -126,12 +126,28 @@ SearchParams base_params(alaya_index *ix) {
   return p;
 }
 
-uint32_t auto_hash_log2(uint32_t ef) {
-  return std::min<uint32_t>(14, std::max<uint32_t>(11, ceil_log2(32ull * ef)));
+constexpr size_t kLdsPerCu = 160 * 1024;
+
+// Size the LDS visited table for residency: the batch wants ceil(nq / CUs) resident queries per
+// CU (capped by what the register file admits); the table takes what LDS is left per query,
+// never more than ~2x the expected visited count (~24 ids per expansion x ef), never below
+// 1024 slots.  A query that outgrows its table spills to the global bitset (exact either way).
+uint32_t auto_hash_log2(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef) {
+  const size_t fixed = alaya_amd::search_lds_bytes(ix->stride, ef, 0) - 4;
+  int vgpr_blocks = 0;
+  hip_check(alaya_amd::search_occupancy(p, fixed + 4096, &vgpr_blocks), "occupancy");
+  vgpr_blocks = std::max(1, vgpr_blocks);
+  const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_blocks, want));
+  const size_t budget = kLdsPerCu / blocks > fixed ? kLdsPerCu / blocks - fixed : 0;
+  uint32_t l = 10;
+  while (l < 15 && (static_cast<size_t>(4) << (l + 1)) <= budget) ++l;
+  return std::max<uint32_t>(10, std::min<uint32_t>(l, ceil_log2(48ull * ef)));
 }
 
 void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t ef,
-               uint32_t *d_ids, float *d_dists, uint32_t *d_cnt, hipStream_t stream) {
+               uint32_t *d_ids, float *d_dists, uint32_t *d_cnt, hipStream_t stream,
+               uint64_t *d_stamps = nullptr) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
   if (!ix->has_graph) throw ArgError("index has no graph");
   if (ef == 0) throw ArgError("ef must be >= 1");
@@ -156,7 +172,8 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   p.out_ids = d_ids;
   p.out_dists = d_dists;
   p.out_counters = d_cnt;
-  p.hash_log2 = ix->hash_log2_override ? ix->hash_log2_override : auto_hash_log2(ef);
+  p.stamps = d_stamps;
+  p.hash_log2 = ix->hash_log2_override ? ix->hash_log2_override : auto_hash_log2(ix, p, nq, ef);
   const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2);
   if (lds > 160 * 1024) throw ArgError("ef / dim too large for the LDS budget");
   int per_cu = 0;
@@ -418,6 +435,30 @@ int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq,
     if (counters)
       hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");
     hip_check(hipStreamSynchronize(ix->stream), "search");
+  });
+}
+
+int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
+                               uint32_t ef, uint32_t *ids, uint32_t *counters, uint64_t *stamps) {
+  return guarded([&] {
+    if (!ix || (nq && (!queries || !ids || !stamps))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (nq == 0 || k == 0) return;
+    ix->q_buf.reserve(nq * ix->dim * 4);
+    ix->id_buf.reserve(nq * k * 4);
+    ix->cnt_buf.reserve(nq * 16);
+    DevBuf st;
+    st.reserve(nq * 64);
+    hip_check(hipMemsetAsync(st.ptr, 0, nq * 64, ix->stream), "memset");
+    hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
+    do_search(ix, ix->q_buf.as<float>(), nq, k, ef, ix->id_buf.as<uint32_t>(), nullptr,
+              ix->cnt_buf.as<uint32_t>(), ix->stream, st.as<uint64_t>());
+    hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    if (counters)
+      hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipMemcpyAsync(stamps, st.ptr, nq * 64, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipStreamSynchronize(ix->stream), "profile search");
   });
 }
 

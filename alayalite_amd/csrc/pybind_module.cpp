@@ -542,6 +542,16 @@ class DeviceIndex {
     return out;
   }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
+  py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
+                           uint32_t ef) {
+    const uint64_t nq = q.shape(0);
+    py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
+    py::array_t<uint32_t> c({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(4)});
+    py::array_t<uint64_t> st({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(8)});
+    check(alaya_index_profile_search(ix_, q.data(), nq, k, ef, ids.mutable_data(), c.mutable_data(),
+                                     st.mutable_data()));
+    return py::make_tuple(ids, c, st);
+  }
   uint64_t device_bytes() const {
     uint64_t b = 0;
     check(alaya_index_info(ix_, nullptr, nullptr, nullptr, nullptr, &b));
@@ -640,6 +650,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("search_device", &DeviceIndex::search_device)
       .def("distances", &DeviceIndex::distances)
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
+      .def("profile_search", &DeviceIndex::profile_search)
       .def("device_bytes", &DeviceIndex::device_bytes);
   m.def("device_count", [] {
     int c = 0;

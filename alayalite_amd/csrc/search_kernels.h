@@ -41,6 +41,7 @@ struct SearchParams {
   uint32_t *work_counter; // zeroed before each launch
   uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area
   uint32_t hash_log2;     // LDS visited table = 1 << hash_log2 slots
+  uint64_t *stamps;       // nullable: diagnostic per-phase cycle counts, nq x 8
 };
 
 size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2);

@@ -32,8 +32,11 @@ constexpr uint32_t kIdMask = 0x7fffffffu;
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ void wave_sync() {
-  // One workgroup == one wave: the barrier orders LDS traffic between lanes at negligible cost.
-  __syncthreads();
+  // One workgroup == one wave.  LDS instructions of a wave execute in order, so a lane's ds_write
+  // is seen by a later ds_read of any lane; this fence only stops the compiler from reordering LDS
+  // accesses across it and, unlike __syncthreads(), does not drain outstanding global loads.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
@@ -66,8 +69,45 @@ __device__ __forceinline__ void accumulate(const float4 x, const float4 y, float
 }
 
 // --------------------------------------------------------------------------------------------
-// Distance of the query (LDS) to `n` rows listed in ids[0..n) -> out[0..n).  8 lanes per row.
+// Distance of the query (LDS) to `n` rows listed in ids[0..n) -> out[0..n).
+// 8 lanes per row (lane m of the group owns partial sums acc[4m..4m+3]); each lane group of a
+// pass handles kRPL rows, so one pass covers 8*kRPL rows and issues every 128 B row chunk of
+// the pass before the first FMA (all loads of the pass in flight at once).
 // --------------------------------------------------------------------------------------------
+template <bool kIP>
+__device__ __forceinline__ float finish_row(float a0, float a1, float a2, float a3) {
+  // (acc0+acc1) + (acc2+acc3) per lane of the 8-wide vector: lanes m^2 then m^4.
+  a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
+  a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+  // lane m==0 holds v[0..3], lane m==1 holds v[4..7]: s[j] = v[j] + v[j+4]; r = (s0+s1)+(s2+s3)
+  const float s0 = a0 + __shfl_xor(a0, 1), s1 = a1 + __shfl_xor(a1, 1);
+  const float s2 = a2 + __shfl_xor(a2, 1), s3 = a3 + __shfl_xor(a3, 1);
+  return (s0 + s1) + (s2 + s3);
+}
+
+template <bool kIP>
+__device__ __forceinline__ float finish_tail(const SearchParams &p, const float *q, const float *row,
+                                             int tail_begin, float res, uint32_t id) {
+  for (int e = tail_begin; e < static_cast<int>(p.dim); ++e) {
+    if (kIP) {
+      res = fmaf(q[e], row[e], res);
+    } else {
+      const float d = q[e] - row[e];
+      res = fmaf(d, d, res);
+    }
+  }
+  if (kIP) res = -res;
+  if (p.valid != nullptr && !((p.valid[id >> 5] >> (id & 31)) & 1u)) res = FLT_MAX;
+  return res;
+}
+
+// rows per lane group per pass for a compile-time chunk count: keep the hoisted row chunks
+// within ~96 float4 (384 VGPRs) -- one wave per SIMD has the whole 512-entry register file.
+template <int kChunks>
+constexpr int rows_per_group() {
+  return kChunks <= 0 ? 1 : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
+}
+
 template <bool kIP, int kChunks>
 __device__ __forceinline__ void row_distances(const SearchParams &p, const float *q,
                                               const uint32_t *ids, int n, float *out) {
@@ -77,59 +117,78 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
   const int rem = static_cast<int>(p.dim) - 32 * T;
   const int nb8 = rem >> 3;
   const int tail_begin = 32 * T + 8 * nb8;
-  for (int base = 0; base < n; base += 8) {
-    const int r = base + g;
-    const bool act = r < n;
-    const uint32_t id = act ? ids[r] : 0u;
-    const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    if (act) {
-      const float4 *rp = reinterpret_cast<const float4 *>(row) + m;
-      const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
-      if constexpr (kChunks > 0) {
+  if constexpr (kChunks > 0) {
+    constexpr int kRPL = rows_per_group<kChunks>();
+    for (int base = 0; base < n; base += 8 * kRPL) {
+      uint32_t id[kRPL];
+      bool act[kRPL];
+      const float *row[kRPL];
+      float4 y[kRPL][kChunks];
 #pragma unroll
-        for (int t = 0; t < kChunks; ++t) {
-          const float4 y = rp[8 * t];
-          const float4 x = qp[8 * t];
-          accumulate<kIP>(x, y, a0, a1, a2, a3);
-        }
-      } else {
-#pragma unroll 6
-        for (int t = 0; t < T; ++t) {
-          const float4 y = rp[8 * t];
-          const float4 x = qp[8 * t];
-          accumulate<kIP>(x, y, a0, a1, a2, a3);
+      for (int r = 0; r < kRPL; ++r) {
+        const int idx = base + g + 8 * r;
+        act[r] = idx < n;
+        id[r] = act[r] ? ids[idx] : 0u;
+        row[r] = p.base + static_cast<uint64_t>(id[r]) * p.stride;
+      }
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) {
+        const float4 *rp = reinterpret_cast<const float4 *>(row[r]) + m;
+        if (act[r]) {
+#pragma unroll
+          for (int t = 0; t < kChunks; ++t) y[r][t] = rp[8 * t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < kChunks; ++t) y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1); rows are 16 B aligned.
-      if (m < 2) {
-        for (int b = 0; b < nb8; ++b) {
-          const int e = 32 * T + 8 * b + 4 * m;
-          const float4 y = *reinterpret_cast<const float4 *>(row + e);
-          const float4 x = *reinterpret_cast<const float4 *>(q + e);
-          accumulate<kIP>(x, y, a0, a1, a2, a3);
+      float a[kRPL][4];
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
+      const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+#pragma unroll
+      for (int t = 0; t < kChunks; ++t) {
+        const float4 x = qp[8 * t];
+#pragma unroll
+        for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
+      }
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) {
+        if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
+          for (int b = 0; b < nb8; ++b) {
+            const int e = 32 * T + 8 * b + 4 * m;
+            if (act[r]) {
+              accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
+                              *reinterpret_cast<const float4 *>(row[r] + e), a[r][0], a[r][1], a[r][2], a[r][3]);
+            }
+          }
         }
+        const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
+        if (act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row[r], tail_begin, res, id[r]);
       }
     }
-    // (acc0+acc1) + (acc2+acc3) per lane of the 8-wide vector: lanes m^2 then m^4.
-    a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
-    a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
-    // lane m==0 holds v[0..3], lane m==1 holds v[4..7]: s[j] = v[j] + v[j+4].
-    const float s0 = a0 + __shfl_xor(a0, 1), s1 = a1 + __shfl_xor(a1, 1);
-    const float s2 = a2 + __shfl_xor(a2, 1), s3 = a3 + __shfl_xor(a3, 1);
-    if (act && m == 0) {
-      float res = (s0 + s1) + (s2 + s3);
-      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e) {
-        if (kIP) {
-          res = fmaf(q[e], row[e], res);
-        } else {
-          const float d = q[e] - row[e];
-          res = fmaf(d, d, res);
+  } else {
+    for (int base = 0; base < n; base += 8) {
+      const int r = base + g;
+      const bool act = r < n;
+      const uint32_t id = act ? ids[r] : 0u;
+      const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      if (act) {
+        const float4 *rp = reinterpret_cast<const float4 *>(row) + m;
+        const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+#pragma unroll 8
+        for (int t = 0; t < T; ++t) accumulate<kIP>(qp[8 * t], rp[8 * t], a0, a1, a2, a3);
+        if (m < 2) {
+          for (int b = 0; b < nb8; ++b) {
+            const int e = 32 * T + 8 * b + 4 * m;
+            accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
+                            *reinterpret_cast<const float4 *>(row + e), a0, a1, a2, a3);
+          }
         }
       }
-      if (kIP) res = -res;
-      if (p.valid != nullptr && !((p.valid[id >> 5] >> (id & 31)) & 1u)) res = FLT_MAX;
-      out[r] = res;
+      const float res = finish_row<kIP>(a0, a1, a2, a3);
+      if (act && m == 0) out[r] = finish_tail<kIP>(p, q, row, tail_begin, res, id);
     }
   }
   wave_sync();
@@ -298,7 +357,10 @@ __device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L) {
 // --------------------------------------------------------------------------------------------
 // The search kernel.
 // --------------------------------------------------------------------------------------------
-template <bool kIP, int kChunks>
+// kStamp: diagnostic build that accumulates s_memtime cycles per phase into p.stamps (nq x 8):
+// [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
+// [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] unused.
+template <bool kIP, int kChunks, bool kStamp>
 __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
@@ -329,6 +391,16 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     qi = __shfl(qi, 0);
     if (qi >= p.nq) break;
 
+    uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = kStamp ? __builtin_readcyclecounter() : 0;
+    const uint64_t t_begin = t_prev;
+    auto stamp = [&](int slot) {
+      if constexpr (kStamp) {
+        const uint64_t now = __builtin_readcyclecounter();
+        st[slot] += now - t_prev;
+        t_prev = now;
+      }
+    };
     // ---- per-query init ------------------------------------------------------------------
     const float *qsrc = p.queries + static_cast<uint64_t>(qi) * p.q_stride;
     for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
@@ -417,9 +489,12 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     }
 
     // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
+    stamp(0);
     while (ps.cur < ps.size) {
       const uint32_t u = pool_pop(ps, L);
       ++n_expand;
+      if (kStamp && vs.spilled) st[5]++;
+      stamp(1);
       const uint32_t *adj = p.l0 + static_cast<uint64_t>(u) * p.R;
       uint32_t v = lane < static_cast<int>(p.R) ? adj[lane] : kEmpty;
       const uint64_t endm = ballot(lane < static_cast<int>(p.R) && v == kEmpty);
@@ -435,18 +510,21 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       const bool fresh = visit(vs, v, act);
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
+      stamp(2);
       if (nf == 0) continue;
       // compact fresh ids in adjacency order
       const uint32_t slot = __popcll(fm & ((1ull << lane) - 1ull));
       if (fresh) L.cid[slot] = v;
       wave_sync();
       row_distances<kIP, kChunks>(p, L.q, L.cid, nf, L.cd);
+      stamp(3);
       n_dist += nf;
       const bool has = lane < nf;
       const uint32_t cid = has ? L.cid[lane] : 0u;
       const float cd = has ? L.cd[lane] : 0.f;
       wave_sync();
       pool_merge(ps, L, has, cid, cd);
+      stamp(4);
     }
 
     // ---- results (ids[i] = pool.id(i), distances[i] = pool.dist(i)) --------------------------
@@ -466,6 +544,10 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       c[1] = n_expand;
       c[2] = n_dist_up;
       c[3] = n_hops_up;
+    }
+    if constexpr (kStamp) {
+      st[6] = __builtin_readcyclecounter() - t_begin;
+      if (lane < 8) p.stamps[static_cast<uint64_t>(qi) * 8 + lane] = st[lane & 7];
     }
     wave_sync();
   }
@@ -502,13 +584,18 @@ size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2) {
          (static_cast<size_t>(1) << hash_log2) * 4;
 }
 
-template <bool kIP, int kChunks>
+template <bool kIP, int kChunks, bool kStamp = false>
 static const void *kernel_ptr() {
-  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks>);
+  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kStamp>);
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim) {
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped) {
   const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
+  if (stamped) {
+    if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();
+    if (chunks == 4) return ip ? kernel_ptr<true, 4, true>() : kernel_ptr<false, 4, true>();
+    return ip ? kernel_ptr<true, 0, true>() : kernel_ptr<false, 0, true>();
+  }
 #define ALAYA_CASE(C)                                                        \
   if (chunks == C) return ip ? kernel_ptr<true, C>() : kernel_ptr<false, C>();
   ALAYA_CASE(4)
@@ -522,7 +609,7 @@ const void *search_kernel_symbol(bool ip, uint32_t dim) {
 }
 
 hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, lds, stream);
@@ -541,7 +628,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 }
 
 hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, lds);
 }
 

@@ -129,7 +129,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from alayalite_amd import _native
-    from bench.datasets import gist_like
+    from workloads.datasets import gist_like
 
     native = _native._ext
     threads = args.build_threads or host_threads()

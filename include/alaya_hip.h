@@ -91,6 +91,11 @@ int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uin
 /* out[q*n + i] = metric distance(queries[q], row ids[i]), bit-exact with the search kernel. */
 int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, const uint32_t *ids,
                           uint32_t n, float *out);
+/* Diagnostic build of the search kernel: also returns per-query s_memtime cycles per phase,
+ * stamps[nq*8] = (init+descent, pop, adjacency+visited, distances, merge, expansions after the
+ * visited table spilled, whole query, 0). Same ids as alaya_index_batch_search. */
+int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
+                               uint32_t ef, uint32_t *ids, uint32_t *counters, uint64_t *stamps);
 /* Tuning / introspection: LDS visited-table size (log2 slots; 0 = automatic). */
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots);
 int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,

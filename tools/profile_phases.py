@@ -1,0 +1,61 @@
+"""Per-phase cycle breakdown of the search kernel (diagnostic build with s_memtime stamps).
+
+usage: python tools/profile_phases.py [--n 1000000] [--ef 400] [--nq 1000] [--hash-log2 0]
+Prints mean cycles per query for init/descent, pop, adjacency+visited, distances, merge, the
+number of expansions after the LDS visited table spilled, and the whole query; and the per-phase
+cycles per expansion.  Read the shares, not the absolute time (stamps perturb the schedule).
+"""
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--dim", type=int, default=960)
+    ap.add_argument("--ef", type=int, default=400)
+    ap.add_argument("--hash-log2", type=int, default=0)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    import bench as b
+    from alayalite_amd import _native
+    from workloads.datasets import gist_like
+
+    ext = _native._ext
+    base, queries = gist_like(args.n, args.nq, args.dim)
+    g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
+    dev = ext.DeviceIndex(0)
+    dev.set_base(base, 0)
+    dev.set_graph(g)
+    if args.hash_log2:
+        dev.set_hash_log2(args.hash_log2)
+    ids0, _, cnt0 = dev.search(queries, 10, args.ef)
+    t = time.time()
+    ids0, _, cnt0 = dev.search(queries, 10, args.ef)
+    plain = time.time() - t
+    ids, cnt, st = dev.profile_search(queries, 10, args.ef)
+    assert np.array_equal(ids, ids0)
+    names = ["init+descent", "pop", "adj+visited", "distances", "merge", "spilled_expansions", "query_total"]
+    mean = st.mean(0)
+    exp = cnt[:, 1].mean()
+    print(f"n={args.n} ef={args.ef} nq={args.nq} host-timed plain search {plain*1e3:.2f} ms "
+          f"mean n_dist={cnt[:,0].mean():.1f} n_expand={exp:.1f}")
+    for i, nme in enumerate(names):
+        per = mean[i] / exp if i not in (5, 6) else mean[i]
+        print(f"  {nme:20s} mean/query {mean[i]:14.1f}   per expansion {mean[i]/exp:10.1f}")
+    print(f"  max query_total {st[:,6].max()}  min {st[:,6].min()}  p50 {np.median(st[:,6])}")
+    if args.out:
+        np.save(args.out, st)
+
+
+if __name__ == "__main__":
+    main()
