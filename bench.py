@@ -129,6 +129,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from alayalite_amd import _native
+    from alayalite_amd.sharded import exchange_and_merge, shard_range
     from workloads.datasets import gist_like
 
     native = _native._ext
@@ -140,8 +141,7 @@ def main():
 
     # ---- index (shard or replica) ------------------------------------------------------------
     if world > 1 and args.mode == "shard":
-        per = (args.n + world - 1) // world
-        lo, hi = rank * per, min(args.n, (rank + 1) * per)
+        lo, hi = shard_range(args.n, world, rank)
         my_base = np.ascontiguousarray(base[lo:hi])
         tag = f"gist_shard{rank}of{world}"
     else:
@@ -164,19 +164,7 @@ def main():
         index.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
                             cnt_dev.data_ptr(), stream.cuda_stream)
         if world > 1 and args.mode == "shard":
-            gid = ids_dev.to(torch.int64) + lo
-            g_ids = [torch.empty_like(gid) for _ in range(world)]
-            g_d = [torch.empty_like(dists_dev) for _ in range(world)]
-            dist.all_gather(g_ids, gid)
-            dist.all_gather(g_d, dists_dev)
-            all_ids = torch.cat(g_ids, 1)
-            all_d = torch.cat(g_d, 1)
-            # merge by (distance asc, global id asc): stable sort by id, then by distance
-            o1 = torch.sort(all_ids, dim=1, stable=True).indices
-            all_ids = torch.gather(all_ids, 1, o1)
-            all_d = torch.gather(all_d, 1, o1)
-            o2 = torch.sort(all_d, dim=1, stable=True).indices[:, :K]
-            return torch.gather(all_ids, 1, o2), torch.gather(all_d, 1, o2)
+            return exchange_and_merge(ids_dev, dists_dev, lo, K)
         return ids_dev, dists_dev
 
     # ---- ground truth + operating point ------------------------------------------------------
@@ -222,17 +210,8 @@ def main():
                             cnt_dev.data_ptr(), stream.cuda_stream)
         ev[i][1].record(stream)
         if world > 1 and args.mode == "shard":
-            # exchange + merge of the same step (search above is the per-shard kernel)
-            gid = ids_dev.to(torch.int64) + lo
-            g_ids = [torch.empty_like(gid) for _ in range(world)]
-            g_d = [torch.empty_like(dists_dev) for _ in range(world)]
-            dist.all_gather(g_ids, gid)
-            dist.all_gather(g_d, dists_dev)
-            all_ids = torch.cat(g_ids, 1)
-            all_d = torch.cat(g_d, 1)
-            o1 = torch.sort(all_ids, dim=1, stable=True).indices
-            o2 = torch.sort(torch.gather(all_d, 1, o1), dim=1, stable=True).indices[:, :K]
-            _ = torch.gather(torch.gather(all_ids, 1, o1), 1, o2)
+            # exchange + merge of the same step (the search above is the per-shard kernel)
+            exchange_and_merge(ids_dev, dists_dev, lo, K)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
