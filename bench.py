@@ -110,6 +110,22 @@ def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64
     return out
 
 
+def pmc_traffic(cfg):
+    """HBM traffic of the search kernel from the committed rocprofv3 PMC passes at this config
+    (tools/run_pmc.sh -> tools/pmc_summary.py -> profiles/r*/traffic.json); None if absent."""
+    import glob
+
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json"))):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if all(t["config"].get(k) == v for k, v in cfg.items()):
+            best = (path, t)
+    return best
+
+
 def recall(ids, gt):
     hits = sum(len(set(ids[i].tolist()) & set(gt[i].tolist())) for i in range(ids.shape[0]))
     return hits / float(ids.size)
@@ -229,6 +245,14 @@ def main():
              + 4 * args.dim + 8 * K)
     bytes_launch = float(per_q.sum())
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    prof = pmc_traffic({"n_base": args.n, "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef})
+    if prof is not None:
+        # measured HBM bytes per algorithmic byte (PMC, gfx950-corrected) x this launch's bytes
+        traffic_bytes = prof[1]["traffic_over_algorithmic"] * bytes_launch
+        traffic = {"gbs": round(traffic_bytes / (kernel_ms * 1e-3) / 1e9, 1),
+                   "bytes_per_launch": int(traffic_bytes),
+                   "source": os.path.relpath(prof[0], ROOT)}
     if args.dump_counters and rank == 0:
         np.save(args.dump_counters, cnt)
 
@@ -279,7 +303,10 @@ def main():
                        "parallelism": f"{args.mode}{world}" if world > 1 else "1gpu",
                        "graph_build_s": round(build_s, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic["gbs"] if traffic else None,
+                         "traffic_bytes_per_launch": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
                          "kernel": "hnsw_search_kernel", "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": int(bytes_launch),
                          "mean_n_dist": round(float(cnt[:, 0].mean()), 1),

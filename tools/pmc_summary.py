@@ -1,0 +1,58 @@
+"""Summarise rocprofv3 --pmc passes (tools/run_pmc.sh) for hnsw_search_kernel into a traffic
+record bench.py reports as roofline.traffic.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KB) counts 128 B requests as 64 B for
+wide coalesced reads -> bytes_read = 2 * FETCH_SIZE * 1024 (cross-checked: TCC_EA0_RDREQ_sum * 64
+equals FETCH_SIZE * 1024 when TCC_EA0_RDREQ_32B_sum == 0).  WRITE_SIZE (KB) is taken as is.
+usage: python tools/pmc_summary.py gpurun_out profiles/r01/traffic.json
+"""
+
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_launch(path, kernel="hnsw_search_kernel"):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"]:
+            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def main(src, dst):
+    c = {}
+    launches = {}
+    for f in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
+        v, n = per_launch(f)
+        c.update(v)
+        launches.update(n)
+    cfg = json.load(open(os.path.join(src, "pmc_FETCH_SIZE.json")))
+    read_b = 2.0 * c["FETCH_SIZE"] * 1024.0
+    write_b = c.get("WRITE_SIZE", 0.0) * 1024.0
+    alg = cfg["roofline"]["algorithmic_bytes_per_launch"]
+    hit = c.get("TCC_HIT_sum", 0.0)
+    miss = c.get("TCC_MISS_sum", 0.0)
+    out = {
+        "kernel": "hnsw_search_kernel",
+        "config": {k: cfg["config"][k] for k in ("n_base", "n_queries", "dim", "k", "ef_search")},
+        "launches_per_pass": launches,
+        "counters_per_launch": c,
+        "hbm_read_bytes_per_launch": read_b,
+        "hbm_write_bytes_per_launch": write_b,
+        "traffic_bytes_per_launch": read_b + write_b,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (read_b + write_b) / alg,
+        "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
+        "rdreq_x64_over_fetch": (c.get("TCC_EA0_RDREQ_sum", 0.0) * 64.0) / (c["FETCH_SIZE"] * 1024.0),
+        "profiled_kernel_ms": cfg["roofline"]["kernel_ms"],
+    }
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    json.dump(out, open(dst, "w"), indent=2)
+    print(json.dumps(out, indent=2))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
