@@ -8,7 +8,9 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hnsw_build.h"
@@ -100,6 +102,11 @@ struct alaya_index {
   bool has_overlay = false, dedup = false;
   DevBuf l0, levels, upper_off, upper_edges, eps;
   uint64_t graph_n = 0;
+  // SQ8 search space
+  bool has_sq8 = false;
+  int sq8_order = 2;
+  uint32_t code_stride = 0;
+  DevBuf codes, sq_min, sq_max, rr_q_buf;
   // scratch
   DevBuf work, overflow, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
   uint32_t hash_log2_override = 0;
@@ -107,7 +114,7 @@ struct alaya_index {
   hipStream_t stream = nullptr;
   uint64_t device_bytes() const {
     return base.bytes + valid.bytes + l0.bytes + levels.bytes + upper_off.bytes +
-           upper_edges.bytes + eps.bytes + overflow.bytes;
+           upper_edges.bytes + eps.bytes + overflow.bytes + codes.bytes + sq_min.bytes + sq_max.bytes;
   }
 };
 
@@ -133,7 +140,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 // never more than ~2x the expected visited count (~24 ids per expansion x ef), never below
 // 1024 slots.  A query that outgrows its table spills to the global bitset (exact either way).
 uint32_t auto_hash_log2(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef) {
-  const size_t fixed = alaya_amd::search_lds_bytes(ix->stride, ef, 0) - 4;
+  const size_t fixed = alaya_amd::search_lds_bytes(ix->stride, ef, 0, p.sq8_order != 0) - 4;
   int vgpr_blocks = 0;
   hip_check(alaya_amd::search_occupancy(p, fixed + 4096, &vgpr_blocks), "occupancy");
   vgpr_blocks = std::max(1, vgpr_blocks);
@@ -147,7 +154,7 @@ uint32_t auto_hash_log2(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t 
 
 void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t ef,
                uint32_t *d_ids, float *d_dists, uint32_t *d_cnt, hipStream_t stream,
-               uint64_t *d_stamps = nullptr) {
+               uint64_t *d_stamps = nullptr, bool sq8 = false) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
   if (!ix->has_graph) throw ArgError("index has no graph");
   if (ef == 0) throw ArgError("ef must be >= 1");
@@ -173,8 +180,17 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   p.out_dists = d_dists;
   p.out_counters = d_cnt;
   p.stamps = d_stamps;
+  if (sq8) {
+    if (!ix->has_sq8) throw ArgError("index has no SQ8 codes");
+    p.sq8_order = ix->sq8_order;
+    p.codes = ix->codes.as<uint8_t>();
+    p.code_stride = ix->code_stride;
+    p.sq_min = ix->sq_min.as<float>();
+    p.sq_max = ix->sq_max.as<float>();
+    p.stamps = nullptr;
+  }
   p.hash_log2 = ix->hash_log2_override ? ix->hash_log2_override : auto_hash_log2(ix, p, nq, ef);
-  const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2);
+  const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2, sq8);
   if (lds > 160 * 1024) throw ArgError("ef / dim too large for the LDS budget");
   int per_cu = 0;
   hip_check(alaya_amd::search_occupancy(p, lds, &per_cu), "occupancy");
@@ -486,6 +502,126 @@ int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, co
                                               ix->stream), "distance launch");
     hip_check(hipMemcpyAsync(out, ix->dout_buf.ptr, nq * n * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     hip_check(hipStreamSynchronize(ix->stream), "distances");
+  });
+}
+
+// ---- SQ8 (space/quant/sq8.hpp:78-143, space/sq8_space.hpp) --------------------------------
+int alaya_sq8_train(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v) {
+  return guarded([&] {
+    if ((n && !data) || !min_v || !max_v || dim == 0) throw ArgError("invalid arguments");
+    for (uint32_t j = 0; j < dim; ++j) {  // SQ8Quantizer ctor: min = max(), max = lowest()
+      min_v[j] = std::numeric_limits<float>::max();
+      max_v[j] = std::numeric_limits<float>::lowest();
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+      const float *r = data + i * dim;
+      for (uint32_t j = 0; j < dim; ++j) {
+        if (r[j] < min_v[j]) min_v[j] = r[j];
+        if (r[j] > max_v[j]) max_v[j] = r[j];
+      }
+    }
+  });
+}
+
+int alaya_sq8_encode(const float *data, uint64_t n, uint32_t dim, const float *min_v,
+                     const float *max_v, uint8_t *codes, uint32_t num_threads) {
+  return guarded([&] {
+    if ((n && (!data || !codes)) || !min_v || !max_v) throw ArgError("invalid arguments");
+    auto work = [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) {
+        for (uint32_t j = 0; j < dim; ++j) {  // SQ8Quantizer::quantize (sq8.hpp:118-130)
+          const float v = data[i * dim + j], mn = min_v[j], mx = max_v[j];
+          uint8_t c;
+          if (mx == mn) c = 0;
+          else if (v >= mx) c = 255;
+          else if (v <= mn) c = 0;
+          else c = static_cast<uint8_t>(((v - mn) / (mx - mn)) * 255);
+          codes[i * dim + j] = c;
+        }
+      }
+    };
+    const uint32_t nt = std::max(1u, std::min<uint32_t>(num_threads, 64));
+    std::vector<std::thread> ts;
+    const uint64_t per = (n + nt - 1) / nt;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint64_t lo = t * per, hi = std::min(n, lo + per);
+      if (lo < hi) ts.emplace_back(work, lo, hi);
+    }
+    for (auto &t : ts) t.join();
+  });
+}
+
+int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint32_t dim,
+                        const float *min_v, const float *max_v, int order) {
+  return guarded([&] {
+    if (!ix || (n && !codes) || !min_v || !max_v) throw ArgError("invalid arguments");
+    if (order != 1 && order != 2) throw ArgError("SQ8 order must be 1 (AVX2) or 2 (AVX-512)");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (ix->base.ptr && (dim != ix->dim || n != ix->n)) throw ArgError("SQ8 codes do not match the base rows");
+    const uint32_t cs = (dim + 63) / 64 * 64;
+    ix->codes.release();
+    ix->codes.reserve(std::max<uint64_t>(n, 1) * cs);
+    if (n) {
+      hip_check(hipMemsetAsync(ix->codes.ptr, 0, n * cs, ix->stream), "memset");
+      hip_check(hipMemcpy2DAsync(ix->codes.ptr, cs, codes, dim, dim, n, hipMemcpyHostToDevice, ix->stream),
+                "upload codes");
+    }
+    ix->sq_min.release();
+    ix->sq_max.release();
+    ix->sq_min.reserve(dim * 4);
+    ix->sq_max.reserve(dim * 4);
+    hip_check(hipMemcpyAsync(ix->sq_min.ptr, min_v, dim * 4, hipMemcpyHostToDevice, ix->stream), "upload");
+    hip_check(hipMemcpyAsync(ix->sq_max.ptr, max_v, dim * 4, hipMemcpyHostToDevice, ix->stream), "upload");
+    hip_check(hipStreamSynchronize(ix->stream), "sync");
+    ix->code_stride = cs;
+    ix->sq8_order = order;
+    ix->has_sq8 = true;
+  });
+}
+
+int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
+                                 uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
+                                 float *dists, uint32_t *counters) {
+  return guarded([&] {
+    if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (nq == 0 || k == 0) return;
+    ix->q_buf.reserve(nq * ix->dim * 4);
+    ix->id_buf.reserve(nq * k * 4);
+    ix->dist_buf.reserve(nq * k * 4);
+    ix->cnt_buf.reserve(nq * 16);
+    hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
+    do_search(ix, ix->q_buf.as<float>(), nq, k, ef, ix->id_buf.as<uint32_t>(), ix->dist_buf.as<float>(),
+              ix->cnt_buf.as<uint32_t>(), ix->stream, nullptr, true);
+    uint32_t *final_ids = ix->id_buf.as<uint32_t>();
+    float *final_d = ix->dist_buf.as<float>();
+    if (rerank) {
+      ix->dlist_buf.reserve(nq * k * 4);
+      ix->dout_buf.reserve(nq * k * 4);
+      const float *rq = ix->q_buf.as<float>();
+      if (rerank_queries && rerank_queries != queries) {
+        ix->rr_q_buf.reserve(nq * ix->dim * 4);
+        hip_check(hipMemcpyAsync(ix->rr_q_buf.ptr, rerank_queries, nq * ix->dim * 4, hipMemcpyHostToDevice,
+                                 ix->stream), "H2D");
+        rq = ix->rr_q_buf.as<float>();
+      }
+      SearchParams p = base_params(ix);
+      p.queries = rq;
+      p.nq = nq;
+      p.q_stride = ix->dim;
+      alaya_amd::RerankParams r{ix->id_buf.as<uint32_t>(), k, ef, ix->dlist_buf.as<uint32_t>(),
+                                ix->dout_buf.as<float>()};
+      hip_check(alaya_amd::launch_rerank(p, r, ix->stream), "rerank launch");
+      final_ids = ix->dlist_buf.as<uint32_t>();
+      final_d = ix->dout_buf.as<float>();
+    }
+    hip_check(hipMemcpyAsync(ids, final_ids, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    if (dists) hip_check(hipMemcpyAsync(dists, final_d, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    if (counters)
+      hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipStreamSynchronize(ix->stream), "sq8 search");
   });
 }
 

@@ -80,6 +80,10 @@ void to_float(const void *src, DType t, size_t count, float *dst) {
   }
 }
 
+// get_l2_sqr_sq8_func / get_ip_sqr_sq8_func pick the AVX-512 kernel on AVX-512F hosts, else AVX2
+// (distance_l2.ipp:694-708): the device reproduces the order this host's reference build uses.
+int host_sq8_order() { return __builtin_cpu_supports("avx512f") ? 2 : 1; }
+
 class PyIndexInterface {
  public:
   explicit PyIndexInterface(const IndexParams &params) : params_(params) {
@@ -132,6 +136,7 @@ class PyIndexInterface {
       check(alaya_graph_build_hnsw(rows_f32_.data(), n, dim_, metric_code(), params_.max_nbrs_,
                                    ef_construction, num_threads, 100, &graph_));
     }
+    if (params_.quantization_type_ == QuantizationType::SQ8) train_sq8(num_threads);
     upload();
   }
 
@@ -265,6 +270,11 @@ class PyIndexInterface {
     if (static_cast<uint32_t>(queries.shape(1)) != dim_) throw py::value_error("query dimension mismatch");
     py::array arr = py::array::ensure(queries, py::array::c_style);
     const uint64_t nq = arr.shape(0);
+    raw_queries_.clear();
+    if (params_.quantization_type_ == QuantizationType::SQ8 && params_.metric_ == MetricType::COS) {
+      raw_queries_.resize(nq * dim_);
+      to_float(arr.data(), dtype_, nq * dim_, raw_queries_.data());
+    }
     if (params_.metric_ == MetricType::COS) normalize_in_place(arr, nq);  // raw_space.hpp:267-269
     py::array_t<float> qf({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(dim_)});
     to_float(arr.data(), dtype_, nq * dim_, qf.mutable_data());
@@ -279,9 +289,20 @@ class PyIndexInterface {
     py::array_t<float> dists({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(topk)});
     last_counters_.assign(nq * 4, 0);
     if (params_.quantization_type_ == QuantizationType::SQ8) {
-      throw std::runtime_error("SQ8 search is not wired on the MI355X engine yet");
-    }
-    {
+      // SQ8Space::QueryComputer encodes the query as given (no COS normalisation), the rerank's
+      // RawSpace::QueryComputer normalises it (raw_space.hpp:267-269): keep both forms.
+      const float *rq = static_cast<const float *>(q.data());
+      const float *sq = raw_queries_.empty() ? rq : raw_queries_.data();
+      // batch_search reranks (index.hpp:337-345); batch_search_with_distance does not and returns
+      // an empty distance array for SQ spaces (index.hpp:391-418, get_topk_array of no rows).
+      const int rerank = want_dist ? 0 : 1;
+      {
+        py::gil_scoped_release nogil;
+        check(alaya_index_batch_search_sq8(ix_, sq, rq, nq, topk, ef, rerank, ids32.data(),
+                                           dists.mutable_data(), last_counters_.data()));
+      }
+      if (want_dist) dists = py::array_t<float>(std::vector<py::ssize_t>{0, static_cast<py::ssize_t>(topk)});
+    } else {
       py::gil_scoped_release nogil;
       check(alaya_index_batch_search(ix_, static_cast<const float *>(q.data()), nq, topk, ef,
                                      ids32.data(), dists.mutable_data(), last_counters_.data()));
@@ -304,6 +325,18 @@ class PyIndexInterface {
     check(alaya_index_set_base(ix_, rows_f32_.data(), n_, dim_, metric_code(),
                                valid_.empty() ? nullptr : valid_.data()));
     check(alaya_index_set_graph(ix_, graph_));
+    if (!sq_codes_.empty())
+      check(alaya_index_set_sq8(ix_, sq_codes_.data(), n_, dim_, sq_min_.data(), sq_max_.data(), host_sq8_order()));
+  }
+
+  void train_sq8(uint32_t num_threads) {
+    if (params_.metric_ == MetricType::COS && dtype_ != kF32) throw std::runtime_error("COS metric only support float or double");
+    sq_min_.assign(dim_, 0.f);
+    sq_max_.assign(dim_, 0.f);
+    sq_codes_.assign(n_ * dim_, 0);
+    check(alaya_sq8_train(rows_f32_.data(), n_, dim_, sq_min_.data(), sq_max_.data()));
+    check(alaya_sq8_encode(rows_f32_.data(), n_, dim_, sq_min_.data(), sq_max_.data(), sq_codes_.data(),
+                           std::max(1u, num_threads)));
   }
 
   // RawSpace save/load (raw_space.hpp:219-250) + SequentialStorage (sequential_storage.hpp:110-142)
@@ -398,8 +431,77 @@ class PyIndexInterface {
     to_float(raw_.data(), dtype_, n_ * dim_, rows_f32_.data());
   }
 
-  void save_sq8(const std::string &) const { throw std::runtime_error("SQ8 save not wired yet"); }
-  void load_sq8(const std::string &) { throw std::runtime_error("SQ8 load not wired yet"); }
+  // SQ8Space save/load (sq8_space.hpp:213-251) + SQ8Quantizer (sq8.hpp:161-177)
+  void save_sq8(const std::string &path) const {
+    std::ofstream w(path, std::ios::binary);
+    if (!w.is_open()) throw std::runtime_error("Cannot open file " + path);
+    const int32_t metric = static_cast<int32_t>(params_.metric_);
+    const uint32_t data_size = dim_;
+    const uint64_t cap = std::max<uint64_t>(params_.capacity_, n_);
+    w.write(reinterpret_cast<const char *>(&metric), 4);
+    w.write(reinterpret_cast<const char *>(&data_size), 4);
+    w.write(reinterpret_cast<const char *>(&dim_), 4);
+    auto put_id = [&](uint64_t v) {
+      if (id_bytes_ == 4) {
+        uint32_t x = static_cast<uint32_t>(v);
+        w.write(reinterpret_cast<const char *>(&x), 4);
+      } else {
+        w.write(reinterpret_cast<const char *>(&v), 8);
+      }
+    };
+    put_id(n_);
+    put_id(0);
+    put_id(cap);
+    const uint64_t item = dim_, aligned = (item + 63) / 64 * 64, align = 64;
+    w.write(reinterpret_cast<const char *>(&item), 8);
+    w.write(reinterpret_cast<const char *>(&aligned), 8);
+    w.write(reinterpret_cast<const char *>(&cap), 8);
+    w.write(reinterpret_cast<const char *>(&n_), 8);
+    w.write(reinterpret_cast<const char *>(&align), 8);
+    std::vector<char> row(aligned, 0);
+    for (uint64_t i = 0; i < cap; ++i) {
+      std::fill(row.begin(), row.end(), 0);
+      if (i < n_) std::memcpy(row.data(), sq_codes_.data() + i * item, item);
+      w.write(row.data(), static_cast<std::streamsize>(aligned));
+    }
+    std::vector<uint8_t> bitmap((cap + 7) / 8, 0);
+    for (uint64_t i = 0; i < n_; ++i) bitmap[i / 8] |= static_cast<uint8_t>(1u << (i % 8));
+    w.write(reinterpret_cast<const char *>(bitmap.data()), static_cast<std::streamsize>(bitmap.size()));
+    w.write(reinterpret_cast<const char *>(&dim_), 4);
+    w.write(reinterpret_cast<const char *>(sq_min_.data()), dim_ * 4);
+    w.write(reinterpret_cast<const char *>(sq_max_.data()), dim_ * 4);
+    if (!w) throw std::runtime_error("write failed: " + path);
+  }
+  void load_sq8(const std::string &path) {
+    std::ifstream r(path, std::ios::binary);
+    if (!r.is_open()) throw std::runtime_error("Cannot open file " + path);
+    int32_t metric;
+    uint32_t data_size, dim;
+    r.read(reinterpret_cast<char *>(&metric), 4);
+    r.read(reinterpret_cast<char *>(&data_size), 4);
+    r.read(reinterpret_cast<char *>(&dim), 4);
+    r.ignore(3 * id_bytes_);
+    uint64_t hdr[5];
+    r.read(reinterpret_cast<char *>(hdr), sizeof(hdr));
+    if (!r || dim != dim_ || hdr[0] != dim) throw std::runtime_error("SQ8 file does not match the raw data");
+    const uint64_t aligned = hdr[1], cap = hdr[2];
+    sq_codes_.assign(n_ * dim_, 0);
+    std::vector<char> row(aligned);
+    for (uint64_t i = 0; i < cap; ++i) {
+      r.read(row.data(), static_cast<std::streamsize>(aligned));
+      if (!r) throw std::runtime_error("truncated SQ8 file");
+      if (i < n_) std::memcpy(sq_codes_.data() + i * dim_, row.data(), dim_);
+    }
+    r.ignore(static_cast<std::streamsize>((cap + 7) / 8));
+    uint32_t qd = 0;
+    r.read(reinterpret_cast<char *>(&qd), 4);
+    if (qd != dim_) throw std::runtime_error("SQ8 quantizer dimension mismatch");
+    sq_min_.resize(dim_);
+    sq_max_.resize(dim_);
+    r.read(reinterpret_cast<char *>(sq_min_.data()), dim_ * 4);
+    r.read(reinterpret_cast<char *>(sq_max_.data()), dim_ * 4);
+    if (!r) throw std::runtime_error("truncated SQ8 file");
+  }
 
   IndexParams params_;
   DType dtype_ = kF32;
@@ -412,6 +514,9 @@ class PyIndexInterface {
   std::vector<float> rows_f32_;    // float rows uploaded to HBM
   std::vector<uint8_t> valid_;     // empty = all valid
   std::vector<uint32_t> last_counters_;
+  std::vector<float> raw_queries_;   // SQ8 + COS: the un-normalised queries the SQ8 search encodes
+  std::vector<uint8_t> sq_codes_;
+  std::vector<float> sq_min_, sq_max_;
 };
 
 
@@ -541,6 +646,28 @@ class DeviceIndex {
     check(alaya_index_distances(ix_, q.data(), nq, ids.data(), n, out.mutable_data()));
     return out;
   }
+  void set_sq8(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> codes,
+               py::array_t<float, py::array::c_style | py::array::forcecast> mn,
+               py::array_t<float, py::array::c_style | py::array::forcecast> mx, int order) {
+    check(alaya_index_set_sq8(ix_, codes.data(), codes.shape(0), static_cast<uint32_t>(codes.shape(1)),
+                              mn.data(), mx.data(), order));
+  }
+  py::tuple search_sq8(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
+                       uint32_t ef, bool rerank, py::object rerank_queries) {
+    const uint64_t nq = q.shape(0);
+    py::array_t<float, py::array::c_style | py::array::forcecast> rq;
+    const float *rqp = nullptr;
+    if (!rerank_queries.is_none()) {
+      rq = py::array_t<float, py::array::c_style | py::array::forcecast>(rerank_queries);
+      rqp = rq.data();
+    }
+    py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
+    py::array_t<float> d({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
+    py::array_t<uint32_t> c({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(4)});
+    check(alaya_index_batch_search_sq8(ix_, q.data(), rqp, nq, k, ef, rerank ? 1 : 0, ids.mutable_data(),
+                                       d.mutable_data(), c.mutable_data()));
+    return py::make_tuple(ids, d, c);
+  }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
   py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
                            uint32_t ef) {
@@ -650,8 +777,26 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("search_device", &DeviceIndex::search_device)
       .def("distances", &DeviceIndex::distances)
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
+      .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)
+      .def("search_sq8", &DeviceIndex::search_sq8, py::arg("queries"), py::arg("k"), py::arg("ef"),
+           py::arg("rerank") = true, py::arg("rerank_queries") = py::none())
       .def("profile_search", &DeviceIndex::profile_search)
       .def("device_bytes", &DeviceIndex::device_bytes);
+  m.def("sq8_train", [](py::array_t<float, py::array::c_style | py::array::forcecast> data) {
+    const uint32_t d = static_cast<uint32_t>(data.shape(1));
+    py::array_t<float> mn(d), mx(d);
+    check(alaya_sq8_train(data.data(), data.shape(0), d, mn.mutable_data(), mx.mutable_data()));
+    return py::make_tuple(mn, mx);
+  });
+  m.def("sq8_encode", [](py::array_t<float, py::array::c_style | py::array::forcecast> data,
+                         py::array_t<float, py::array::c_style | py::array::forcecast> mn,
+                         py::array_t<float, py::array::c_style | py::array::forcecast> mx, uint32_t threads) {
+    py::array_t<uint8_t> codes({data.shape(0), data.shape(1)});
+    check(alaya_sq8_encode(data.data(), data.shape(0), static_cast<uint32_t>(data.shape(1)), mn.data(), mx.data(),
+                           codes.mutable_data(), threads));
+    return codes;
+  }, py::arg("data"), py::arg("min"), py::arg("max"), py::arg("num_threads") = 1u);
+  m.def("host_sq8_order", &host_sq8_order);
   m.def("device_count", [] {
     int c = 0;
     check(alaya_device_count(&c));

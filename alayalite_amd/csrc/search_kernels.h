@@ -42,9 +42,25 @@ struct SearchParams {
   uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area
   uint32_t hash_log2;     // LDS visited table = 1 << hash_log2 slots
   uint64_t *stamps;       // nullable: diagnostic per-phase cycle counts, nq x 8
+  // SQ8 search space (SQ8Space, space/sq8_space.hpp): traversal distances on uint8 codes
+  int sq8_order;          // 0 = f32 RawSpace search; 2 = AVX-512 SQ8 order; 1 = AVX2 SQ8 order
+  const uint8_t *codes;   // n rows of code_stride bytes (16 B aligned)
+  uint32_t code_stride;
+  const float *sq_min;    // per-dimension min / max of SQ8Quantizer (sq8.hpp:99-113)
+  const float *sq_max;
 };
 
-size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2);
+// PyIndex::rerank inputs (python/include/index.hpp:450-488).
+struct RerankParams {
+  const uint32_t *search_ids;  // nq x k ids written by the SQ8 search
+  uint32_t k, ef;
+  uint32_t *out_ids;           // nq x k
+  float *out_dists;            // nq x k (nullable)
+};
+
+size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8 = false);
+// rerank: p.base/p.queries are the raw f32 rows and the (normalised) f32 queries
+hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream);
 hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu);
 hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream);
 // out[q * n + i] = dist(queries[q], base[ids[i]]) for q < nq (bit-exact device distance)

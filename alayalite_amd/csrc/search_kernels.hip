@@ -53,7 +53,14 @@ struct Lds {
   uint32_t *cid;     // 64 candidate ids (adjacency order)
   float *cd;         // 64 candidate distances
   float *sd;         // 64 sorted accepted distances
+  float *sq_scale;   // SQ8: per-dimension scale (nullptr for f32 search)
+  float *sq_min;     // SQ8: per-dimension min
 };
+
+// Distance of the query to candidate rows in the index's search space.
+template <bool kIP, int kChunks, int kSpace>
+__device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
+                                                const uint32_t *ids, int n, float *out);
 
 template <bool kIP>
 __device__ __forceinline__ void accumulate(const float4 x, const float4 y, float &a0, float &a1,
@@ -192,6 +199,119 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
     }
   }
   wave_sync();
+}
+
+// --------------------------------------------------------------------------------------------
+// SQ8 distances (SQ8Space::QueryComputer over l2_sqr_sq8 / ip_sqr_sq8).  The reference picks the
+// AVX-512 kernel when the host has AVX-512F, else AVX2 (distance_l2.ipp:694-708,
+// distance_ip.ipp:703-716).  Both are "P partial sums, element P*t+j -> acc[j]":
+//   AVX-512 (:334-408 / :292-366): P = 32 (sum0 = acc[0..15], sum1 = acc[16..31]); a trailing
+//     16-block feeds acc[0..15]; combine a = sum0+sum1, then GCC 11 _mm512_reduce_add_ps:
+//     T3[j] = a[8+j]+a[j], T6[j] = T3[4+j]+T3[j], r = (T6[0]+T6[2]) + (T6[1]+T6[3]).
+//   AVX2 (:244-329 / :198-287): P = 16 (sum0 = acc[0..7], sum1 = acc[8..15]); a trailing 8-block
+//     feeds acc[0..7]; combine v = sum0+sum1, s[j] = v[j]+v[j+4], r = (s0+s1)+(s2+s3).
+// Per element: scale = (max-min)*(1/255); L2: d = (x-y)*scale, acc = fma(d,d,acc);
+// IP: xv = fma(x,scale,min), yv = fma(y,scale,min), acc = fma(xv,yv,acc).  Scalar tail the same.
+// Two lanes per row (lane h owns acc[h*P/2 ...]): one pass covers 32 rows.  LDS holds, per
+// dimension, the query term (x for L2, xv for IP), scale and min.
+// --------------------------------------------------------------------------------------------
+template <bool kIP>
+__device__ __forceinline__ float sq8_term(float xq, float scale, float mn, float yf, float acc) {
+  if (kIP) return fmaf(xq, fmaf(yf, scale, mn), acc);
+  const float d = (xq - yf) * scale;
+  return fmaf(d, d, acc);
+}
+
+template <bool kIP, int kOrder, int kFull>
+__device__ __forceinline__ void sq8_distances(const SearchParams &p, const float *xq,
+                                              const float *sc, const float *mnv,
+                                              const uint32_t *ids, int n, float *out) {
+  constexpr int P = kOrder == 2 ? 32 : 16;
+  constexpr int H = P / 2;
+  constexpr int W = H / 4;  // 32-bit words per lane per chunk
+  const int lane = lane_id();
+  const int g = lane >> 1, h = lane & 1;
+  const int T = kFull > 0 ? kFull : static_cast<int>(p.dim) / P;
+  const int rem = static_cast<int>(p.dim) - P * T;
+  const bool half = rem >= H;
+  const int tail_begin = P * T + (half ? H : 0);
+  for (int base = 0; base < n; base += 32) {
+    const int r = base + g;
+    const bool act = r < n;
+    const uint32_t id = act ? ids[r] : 0u;
+    const uint8_t *row = p.codes + static_cast<uint64_t>(id) * p.code_stride;
+    float acc[H];
+#pragma unroll
+    for (int l = 0; l < H; ++l) acc[l] = 0.f;
+    auto chunk = [&](int t, const uint32_t *w, int hh) {
+#pragma unroll
+      for (int l = 0; l < H; ++l) {
+        const int e = P * t + H * hh + l;
+        const float yf = static_cast<float>((w[l >> 2] >> (8 * (l & 3))) & 0xffu);
+        acc[l] = sq8_term<kIP>(xq[e], sc[e], mnv[e], yf, acc[l]);
+      }
+    };
+    if (act) {
+      if constexpr (kFull > 0) {
+        uint32_t w[kFull][W];
+#pragma unroll
+        for (int t = 0; t < kFull; ++t) {
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * t + H * h);
+#pragma unroll
+          for (int q = 0; q < W; ++q) w[t][q] = src[q];
+        }
+#pragma unroll
+        for (int t = 0; t < kFull; ++t) chunk(t, w[t], h);
+      } else {
+        for (int t = 0; t < T; ++t) {
+          uint32_t w[W];
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * t + H * h);
+#pragma unroll
+          for (int q = 0; q < W; ++q) w[q] = src[q];
+          chunk(t, w, h);
+        }
+      }
+      if (half && h == 0) {  // trailing half block -> sum0
+        uint32_t w[W];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * T);
+#pragma unroll
+        for (int q = 0; q < W; ++q) w[q] = src[q];
+        chunk(T, w, 0);
+      }
+    }
+    float res;
+#pragma unroll
+    for (int l = 0; l < H; ++l) acc[l] += __shfl_xor(acc[l], 1);  // sum0 + sum1
+    if constexpr (kOrder == 2) {
+      float t3[8], t6[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t3[j] = acc[8 + j] + acc[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t6[j] = t3[4 + j] + t3[j];
+      res = (t6[0] + t6[2]) + (t6[1] + t6[3]);
+    } else {
+      float s4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s4[j] = acc[j] + acc[j + 4];
+      res = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    }
+    if (act && h == 0) {
+      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
+        res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(row[e]), res);
+      out[r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
+    }
+  }
+  wave_sync();
+}
+
+template <bool kIP, int kChunks, int kSpace>
+__device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
+                                                const uint32_t *ids, int n, float *out) {
+  if constexpr (kSpace == 0) {
+    row_distances<kIP, kChunks>(p, L.q, ids, n, out);
+  } else {
+    sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks>(p, L.q, L.sq_scale, L.sq_min, ids, n, out);
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -360,7 +480,7 @@ __device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L) {
 // kStamp: diagnostic build that accumulates s_memtime cycles per phase into p.stamps (nq x 8):
 // [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
 // [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] unused.
-template <bool kIP, int kChunks, bool kStamp>
+template <bool kIP, int kChunks, bool kStamp, int kSpace = 0>
 __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
@@ -380,6 +500,10 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     L.pi = reinterpret_cast<uint32_t *>(ptr);
     ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
     L.hash = reinterpret_cast<uint32_t *>(ptr);
+    ptr += (static_cast<size_t>(1) << p.hash_log2) * 4;
+    L.sq_scale = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
+    ptr += kSpace ? static_cast<size_t>(p.stride) * 4 : 0;
+    L.sq_min = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
   }
   const uint32_t hsize = 1u << p.hash_log2;
   const uint64_t bit_words = (p.n + 31) / 32;
@@ -403,7 +527,32 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     };
     // ---- per-query init ------------------------------------------------------------------
     const float *qsrc = p.queries + static_cast<uint64_t>(qi) * p.q_stride;
-    for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
+    if constexpr (kSpace == 0) {
+      for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
+    } else {
+      // SQ8Space::QueryComputer encodes the query with the quantizer (sq8_space.hpp:266-271,
+      // SQ8Quantizer::quantize sq8.hpp:118-130), then every distance uses its codes.
+      const float kInv255 = 1.0f / 255.0f;
+      for (uint32_t e = lane; e < p.stride; e += 64) {
+        float xq = 0.f, sc = 0.f, mn = 0.f;
+        if (e < p.dim) {
+          const float v = qsrc[e];
+          mn = p.sq_min[e];
+          const float mx = p.sq_max[e];
+          uint32_t code;
+          if (mx == mn) code = 0;
+          else if (v >= mx) code = 255;
+          else if (v <= mn) code = 0;
+          else code = static_cast<uint8_t>(((v - mn) / (mx - mn)) * 255);
+          sc = (mx - mn) * kInv255;
+          const float xf = static_cast<float>(code);
+          xq = kIP ? fmaf(xf, sc, mn) : xf;
+        }
+        L.q[e] = xq;
+        L.sq_scale[e] = sc;
+        L.sq_min[e] = mn;
+      }
+    }
     for (uint32_t e = lane; e < hsize; e += 64) L.hash[e] = kEmpty;
     for (uint32_t e = lane; e <= p.ef; e += 64) {
       L.pd[e] = 0.f;
@@ -420,7 +569,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       uint32_t u = p.ep;
       if (lane == 0) L.cid[0] = u;
       wave_sync();
-      row_distances<kIP, kChunks>(p, L.q, L.cid, 1, L.cd);
+      space_distances<kIP, kChunks, kSpace>(p, L, L.cid, 1, L.cd);
       float cur = L.cd[0];
       ++n_dist_up;
       for (int level = static_cast<int>(p.levels[u]); level > 0; --level) {
@@ -437,7 +586,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
           wave_sync();
           if (lane < cnt) L.cid[lane] = v;
           wave_sync();
-          row_distances<kIP, kChunks>(p, L.q, L.cid, cnt, L.cd);
+          space_distances<kIP, kChunks, kSpace>(p, L, L.cid, cnt, L.cd);
           n_dist_up += cnt;
           // first index of the minimum == the sequential strict-'<' scan's final choice
           float dl = lane < cnt ? L.cd[lane] : FLT_MAX;
@@ -472,7 +621,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
         if (has) L.cid[lane] = v;
         wave_sync();
         for (uint32_t c = 0; c < cnt; c += 8) {
-          row_distances<kIP, kChunks>(p, L.q, L.cid + c, min(8u, cnt - c), L.cd + c);
+          space_distances<kIP, kChunks, kSpace>(p, L, L.cid + c, min(8u, cnt - c), L.cd + c);
         }
         n_dist_up += cnt;
         const float d = has ? L.cd[lane] : 0.f;
@@ -516,7 +665,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       const uint32_t slot = __popcll(fm & ((1ull << lane) - 1ull));
       if (fresh) L.cid[slot] = v;
       wave_sync();
-      row_distances<kIP, kChunks>(p, L.q, L.cid, nf, L.cd);
+      space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd);
       stamp(3);
       n_dist += nf;
       const bool has = lane < nf;
@@ -577,19 +726,91 @@ __global__ void __launch_bounds__(64) row_distance_kernel(SearchParams p, const 
   }
 }
 
+
+// PyIndex::rerank (python/include/index.hpp:450-488) for SQ8 indexes, Linux batch path (:337-345):
+// res_pool[i] holds the k ids the search wrote plus ef-k zeros; all ef entries are rescored with
+// the raw-space QueryComputer (f32 rows, FLT_MAX for invalid rows) and the k smallest
+// pair<dist, id> are returned (id 0 can repeat -- reference behaviour).  One wave per query.
+template <bool kIP>
+__global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams rp) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float *q = reinterpret_cast<float *>(smem);
+  uint32_t *cid = reinterpret_cast<uint32_t *>(smem + static_cast<size_t>(p.stride) * 4);
+  const uint32_t cap = rp.k + 1;
+  float *cd = reinterpret_cast<float *>(cid + cap);
+  uint32_t *cm = reinterpret_cast<uint32_t *>(cd + cap);
+  const int lane = lane_id();
+  const uint32_t taken = min(rp.k, rp.ef);
+  const uint32_t zeros = rp.ef > rp.k ? rp.ef - rp.k : 0u;
+  const uint32_t c = taken + (zeros ? 1u : 0u);
+  for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
+    const float *qsrc = p.queries + qi * p.q_stride;
+    for (uint32_t e = lane; e < p.stride; e += 64) q[e] = e < p.dim ? qsrc[e] : 0.f;
+    for (uint32_t i = lane; i < c; i += 64) {
+      cid[i] = i < taken ? rp.search_ids[qi * rp.k + i] : 0u;
+      cm[i] = i < taken ? 1u : zeros;
+    }
+    wave_sync();
+    row_distances<kIP, 0>(p, q, cid, static_cast<int>(c), cd);
+    // rank of each distinct entry in the (dist, id) order, equal pairs in entry order
+    for (uint32_t i = lane; i < c; i += 64) {
+      const float di = cd[i];
+      const uint32_t ii = cid[i];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < c; ++j) {
+        const float dj = cd[j];
+        const uint32_t ij = cid[j];
+        const bool less = dj < di || (dj == di && ij < ii);
+        const bool tie_before = dj == di && ij == ii && j < i;
+        if (less || tie_before) rank += cm[j];
+      }
+      for (uint32_t m = 0; m < cm[i] && rank + m < rp.k; ++m) {
+        rp.out_ids[qi * rp.k + rank + m] = ii;
+        if (rp.out_dists) rp.out_dists[qi * rp.k + rank + m] = di;
+      }
+    }
+    for (uint32_t i = taken + zeros + lane; i < rp.k; i += 64) {  // ef < k: nothing left to pop
+      rp.out_ids[qi * rp.k + i] = 0u;
+      if (rp.out_dists) rp.out_dists[qi * rp.k + i] = 0.f;
+    }
+    wave_sync();
+  }
+}
 }  // namespace
 
-size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2) {
+size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8) {
   return static_cast<size_t>(stride) * 4 + 3 * 64 * 4 + 2 * (((ef + 1) * 4 + 15) / 16 * 16) +
-         (static_cast<size_t>(1) << hash_log2) * 4;
+         (static_cast<size_t>(1) << hash_log2) * 4 + (sq8 ? 2 * static_cast<size_t>(stride) * 4 : 0);
 }
 
-template <bool kIP, int kChunks, bool kStamp = false>
+hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream) {
+  const size_t lds = static_cast<size_t>(p.stride) * 4 + 3 * (static_cast<size_t>(r.k) + 1) * 4 + 64;
+  const int grid = static_cast<int>(std::min<uint64_t>(p.nq, 4096));
+  if (p.ip) {
+    hipLaunchKernelGGL(rerank_kernel<true>, dim3(grid), dim3(64), lds, stream, p, r);
+  } else {
+    hipLaunchKernelGGL(rerank_kernel<false>, dim3(grid), dim3(64), lds, stream, p, r);
+  }
+  return hipGetLastError();
+}
+
+template <bool kIP, int kChunks, bool kStamp = false, int kSpace = 0>
 static const void *kernel_ptr() {
-  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kStamp>);
+  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kStamp, kSpace>);
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped) {
+template <int kSpace>
+static const void *sq8_symbol(bool ip, uint32_t dim) {
+  const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
+  if (chunks == 4) return ip ? kernel_ptr<true, 4, false, kSpace>() : kernel_ptr<false, 4, false, kSpace>();
+  if (chunks == 24) return ip ? kernel_ptr<true, 24, false, kSpace>() : kernel_ptr<false, 24, false, kSpace>();
+  if (chunks == 30) return ip ? kernel_ptr<true, 30, false, kSpace>() : kernel_ptr<false, 30, false, kSpace>();
+  return ip ? kernel_ptr<true, 0, false, kSpace>() : kernel_ptr<false, 0, false, kSpace>();
+}
+
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order) {
+  if (sq8_order == 2) return sq8_symbol<2>(ip, dim);
+  if (sq8_order == 1) return sq8_symbol<1>(ip, dim);
   const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
   if (stamped) {
     if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();
@@ -609,7 +830,7 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped) {
 }
 
 hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, lds, stream);
@@ -628,7 +849,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 }
 
 hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, lds);
 }
 

@@ -96,6 +96,22 @@ int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, co
  * visited table spilled, whole query, 0). Same ids as alaya_index_batch_search. */
 int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
                                uint32_t ef, uint32_t *ids, uint32_t *counters, uint64_t *stamps);
+/* ---- SQ8 search space (SQ8Space: include/space/sq8_space.hpp, quant/sq8.hpp) --------------------
+ * Per-dimension min/max (SQ8Quantizer::fit, sq8.hpp:99-113) and codes (quantize, :118-130). */
+int alaya_sq8_train(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v);
+int alaya_sq8_encode(const float *data, uint64_t n, uint32_t dim, const float *min_v,
+                     const float *max_v, uint8_t *codes, uint32_t num_threads);
+/* Attach SQ8 codes (n x dim) to an index whose f32 rows are set.  order: the reduction order of
+ * the reference kernel the host would pick -- 2 = l2/ip_sqr_sq8_avx512 (AVX-512F hosts),
+ * 1 = the AVX2 variants (distance_l2.ipp:694-708, distance_ip.ipp:703-716). */
+int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint32_t dim,
+                        const float *min_v, const float *max_v, int order);
+/* PyIndex::batch_search with SearchSpace = SQ8Space (index.hpp:289-346): graph search on the SQ8
+ * codes (queries encoded in-kernel), then -- if rerank -- PyIndex::rerank on the f32 rows with
+ * rerank_queries (NULL = queries) including its ef-k zero entries (index.hpp:450-488). */
+int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
+                                 uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
+                                 float *dists, uint32_t *counters);
 /* Tuning / introspection: LDS visited-table size (log2 slots; 0 = automatic). */
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots);
 int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,

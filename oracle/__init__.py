@@ -34,6 +34,12 @@ class OrcIndex(C.Structure):
         ("upper_edges", C.c_void_p),
         ("upper_R", C.c_uint32),
         ("ep", C.c_uint32),
+        ("space", C.c_int),
+        ("codes", C.c_void_p),
+        ("code_stride", C.c_uint32),
+        ("sq_min", C.c_void_p),
+        ("sq_max", C.c_void_p),
+        ("sq8_variant", C.c_int),
     ]
 
 
@@ -93,6 +99,7 @@ def lib():
         _lib.orc_batch_search_coro.restype = C.c_double
         _lib.orc_batch_search_coro.argtypes = [
             C.POINTER(OrcIndex), p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, p, p, p]
+        _lib.orc_rerank.argtypes = [C.POINTER(OrcIndex), p, p, C.c_uint32, C.c_uint32, p, p]
         _lib.orc_sq8_fit.argtypes = [p, C.c_uint64, C.c_uint32, p, p]
         _lib.orc_sq8_encode.argtypes = [p, C.c_uint32, p, p, p]
         for name in ("orc_sq8_l2", "orc_sq8_ip"):
@@ -166,7 +173,9 @@ class Pool:
 class IndexView:
     """Host arrays of one index (base rows + HNSW graph) in the layout orc_index expects."""
 
-    def __init__(self, base, l0, levels, upper_off, upper_edges, upper_R, ep, metric=L2, valid=None):
+    def __init__(self, base, l0, levels, upper_off, upper_edges, upper_R, ep, metric=L2, valid=None,
+                 sq8=None):
+        """sq8 = (codes[n, d] uint8, min[d], max[d], variant) switches the search space to SQ8Space."""
         self.base = np.ascontiguousarray(base, np.float32)
         self.l0 = np.ascontiguousarray(l0, np.uint32)
         self.levels = None if levels is None else np.ascontiguousarray(levels, np.uint32)
@@ -180,6 +189,26 @@ class IndexView:
             valid=_ptr(self.valid), metric=metric, l0=_ptr(self.l0), R=self.l0.shape[1],
             levels=_ptr(self.levels), upper_off=_ptr(self.upper_off), upper_edges=_ptr(self.upper_edges),
             upper_R=upper_R, ep=ep)
+        if sq8 is not None:
+            codes, mn, mx, variant = sq8
+            self.codes = np.ascontiguousarray(codes, np.uint8)
+            self.sq_min = np.ascontiguousarray(mn, np.float32)
+            self.sq_max = np.ascontiguousarray(mx, np.float32)
+            self.s.space = 1
+            self.s.codes = _ptr(self.codes)
+            self.s.code_stride = self.codes.shape[1]
+            self.s.sq_min = _ptr(self.sq_min)
+            self.s.sq_max = _ptr(self.sq_max)
+            self.s.sq8_variant = variant
+
+    def rerank(self, query, search_ids, k, ef):
+        """PyIndex::rerank on the raw f32 rows (index.hpp:450-488), Linux batch call shape."""
+        q = np.ascontiguousarray(query, np.float32)
+        src = np.ascontiguousarray(search_ids, np.uint32)
+        ids = np.zeros(k, np.uint32)
+        d = np.zeros(k, np.float32)
+        lib().orc_rerank(C.byref(self.s), _ptr(q), _ptr(src), k, ef, _ptr(ids), _ptr(d))
+        return ids, d
 
     def search(self, query, k, ef, with_counters=False):
         q = np.ascontiguousarray(query, np.float32)

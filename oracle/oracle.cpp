@@ -15,6 +15,7 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <queue>
 #include <thread>
 #include <vector>
 
@@ -203,10 +204,24 @@ struct Pool {
 // QueryComputer (raw_space.hpp:255-305): FLT_MAX for invalid rows, else dist(query, row).
 // COS queries are normalised by the caller (the reference normalises the caller's buffer).
 // ------------------------------------------------------------------------------------------
+float sq8_dist_any(int metric, const uint8_t *x, const uint8_t *y, size_t dim, const float *mn,
+                   const float *mx, int variant);
+void sq8_encode_row(const float *row, uint32_t dim, const float *mn, const float *mx, uint8_t *code);
+
 struct QC {
   const orc_index *ix;
   const float *q;
+  std::vector<uint8_t> qcode;  // SQ8 QueryComputer encodes the query (sq8_space.hpp:266-271)
+  QC(const orc_index *i, const float *query) : ix(i), q(query) {
+    if (ix->space == 1) {
+      qcode.resize(ix->dim);
+      sq8_encode_row(query, ix->dim, ix->sq_min, ix->sq_max, qcode.data());
+    }
+  }
   float operator()(uint32_t u) const {
+    if (ix->space == 1)  // no validity check in SQ8Space::QueryComputer (sq8_space.hpp:290-297)
+      return sq8_dist_any(ix->metric, qcode.data(), ix->codes + static_cast<uint64_t>(u) * ix->code_stride,
+                          ix->dim, ix->sq_min, ix->sq_max, ix->sq8_variant);
     if (ix->valid && !((ix->valid[u >> 3] >> (u & 7)) & 1)) return FLT_MAX;
     return fast_dist(ix->metric, q, ix->base + static_cast<uint64_t>(u) * ix->stride, ix->dim);
   }
@@ -269,7 +284,7 @@ struct Task {
 // suspension after each pop (edge-list prefetch) and before each distance (row prefetch).
 Task search_coro(const orc_index *ix, const float *query, uint32_t k, uint32_t ef, uint32_t *ids,
                  float *dists, orc_counters *cnt) {
-  QC qc{ix, query};
+  QC qc(ix, query);
   Pool pool(ix->n, static_cast<int>(ef));
   initialize_search(ix, pool, qc, cnt);
   while (pool.has_next()) {
@@ -387,6 +402,24 @@ float sq8_dist(const uint8_t *x, const uint8_t *y, size_t dim, const float *mn, 
   return kIP ? -r : r;
 }
 
+float sq8_dist_any(int metric, const uint8_t *x, const uint8_t *y, size_t dim, const float *mn,
+                   const float *mx, int variant) {
+  return metric == ORC_L2 ? sq8_dist<false>(x, y, dim, mn, mx, variant)
+                          : sq8_dist<true>(x, y, dim, mn, mx, variant);
+}
+
+void sq8_encode_row(const float *row, uint32_t dim, const float *mn, const float *mx, uint8_t *code) {
+  for (uint32_t j = 0; j < dim; ++j) {  // SQ8Quantizer::quantize (sq8.hpp:118-130)
+    float v = row[j], lo = mn[j], hi = mx[j];
+    uint8_t c;
+    if (hi == lo) c = 0;
+    else if (v >= hi) c = 255;
+    else if (v <= lo) c = 0;
+    else c = static_cast<uint8_t>(((v - lo) / (hi - lo)) * 255);
+    code[j] = c;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -449,7 +482,7 @@ float orc_pool_dist(const orc_pool *p, size_t i) { return p->p.data[i].dist; }
 // GraphSearchJob::search_solo (graph_search_job.hpp:302-371).
 void orc_search(const orc_index *ix, const float *query, uint32_t k, uint32_t ef, uint32_t *ids,
                 float *dists, orc_counters *cnt) {
-  QC qc{ix, query};
+  QC qc(ix, query);
   Pool pool(ix->n, static_cast<int>(ef));
   initialize_search(ix, pool, qc, cnt);
   while (pool.has_next()) {
@@ -531,14 +564,28 @@ void orc_sq8_fit(const float *data, uint64_t n, uint32_t dim, float *min_v, floa
 
 void orc_sq8_encode(const float *row, uint32_t dim, const float *min_v, const float *max_v,
                     uint8_t *code) {
-  for (uint32_t j = 0; j < dim; ++j) {
-    float v = row[j], mn = min_v[j], mx = max_v[j];
-    uint8_t c;
-    if (mx == mn) c = 0;
-    else if (v >= mx) c = 255;
-    else if (v <= mn) c = 0;
-    else c = static_cast<uint8_t>(((v - mn) / (mx - mn)) * 255);
-    code[j] = c;
+  sq8_encode_row(row, dim, min_v, max_v, code);
+}
+
+void orc_rerank(const orc_index *ix, const float *query, const uint32_t *search_ids, uint32_t k,
+                uint32_t ef, uint32_t *ids, float *dists) {
+  orc_index raw = *ix;
+  raw.space = 0;
+  QC qc(&raw, query);
+  std::vector<uint32_t> src(std::max(ef, k), 0u);  // res_pool(ef): zeros past the k written ids
+  for (uint32_t i = 0; i < k; ++i) src[i] = search_ids[i];
+  std::priority_queue<std::pair<float, uint32_t>, std::vector<std::pair<float, uint32_t>>,
+                      std::greater<>> pq;
+  for (uint32_t i = 0; i < ef; ++i) pq.push({qc(src[i]), src[i]});
+  for (uint32_t i = 0; i < k; ++i) {
+    if (pq.empty()) {
+      ids[i] = 0;
+      dists[i] = 0.0f;
+      continue;
+    }
+    dists[i] = pq.top().first;
+    ids[i] = pq.top().second;
+    pq.pop();
   }
 }
 

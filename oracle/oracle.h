@@ -76,6 +76,12 @@ typedef struct {
   const uint32_t *upper_edges;
   uint32_t upper_R;
   uint32_t ep;
+  /* SQ8 search space (SQ8Space, space/sq8_space.hpp:255-298); used when space == 1 */
+  int space;                  /* 0 = RawSpace (f32 rows), 1 = SQ8Space                          */
+  const uint8_t *codes;       /* n rows of code_stride bytes                                    */
+  uint32_t code_stride;
+  const float *sq_min, *sq_max;
+  int sq8_variant;            /* 0 generic, 1 AVX2, 2 AVX-512 (get_*_sq8_func host choice)       */
 } orc_index;
 
 typedef struct {
@@ -94,6 +100,13 @@ void orc_search(const orc_index *ix, const float *query, uint32_t k, uint32_t ef
 double orc_batch_search_coro(const orc_index *ix, const float *queries, uint64_t nq, uint32_t k,
                              uint32_t ef, uint32_t num_threads, uint32_t *ids, float *dists,
                              orc_counters *cnt);
+
+/* PyIndex::rerank (python/include/index.hpp:450-488) as the Linux batch path calls it (:337-345):
+ * src = the k ids search_job wrote into a zero-initialised ef-sized res_pool (so ef-k extra zeros),
+ * rescored with the raw-space QueryComputer (metric on f32 rows of ix, FLT_MAX for invalid rows),
+ * top-k by a min-heap on pair<dist, id>.  Writes k ids and their distances. */
+void orc_rerank(const orc_index *ix, const float *query, const uint32_t *search_ids, uint32_t k,
+                uint32_t ef, uint32_t *ids, float *dists);
 
 /* ---- SQ8 ---------------------------------------------------------------------------------- */
 void orc_sq8_fit(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v);
