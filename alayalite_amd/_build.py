@@ -25,8 +25,8 @@ ARCH = os.environ.get("ALAYA_OFFLOAD_ARCH", "gfx950")
 LIB = os.path.join(HERE, "libalaya_hip.so")
 EXT = os.path.join(HERE, "_alayalitepy" + sysconfig.get_config_var("EXT_SUFFIX"))
 
-LIB_SOURCES = ["search_kernels.hip", "capi.cpp", "hnsw_build.cpp"]
-LIB_HEADERS = ["search_kernels.h", "hnsw_build.h", "host_distance.h"]
+LIB_SOURCES = ["search_kernels.hip", "flat_kernels.hip", "capi.cpp", "hnsw_build.cpp"]
+LIB_HEADERS = ["search_kernels.h", "flat_kernels.h", "hnsw_build.h", "host_distance.h"]
 EXT_SOURCES = ["pybind_module.cpp"]
 
 
@@ -46,15 +46,20 @@ def _run(cmd: list[str], verbose: bool) -> None:
 def build(force: bool = False, verbose: bool = False) -> tuple[str, str]:
     lib_deps = [os.path.join(CSRC, f) for f in LIB_SOURCES + LIB_HEADERS] + [os.path.join(INCLUDE, "alaya_hip.h")]
     if force or _newer(LIB, lib_deps):
-        objs = []
-        for src in LIB_SOURCES:
+        objs, procs = [], []
+        for src in LIB_SOURCES:  # compile translation units concurrently
             obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
             flags = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-pthread",
                      f"-I{INCLUDE}", "-c", os.path.join(CSRC, src), "-o", obj]
             if src.endswith(".hip"):
                 flags[1:1] = ["-x", "hip", f"--offload-arch={ARCH}"]
-            _run(flags, verbose)
+            if verbose:
+                print(" ".join(flags), flush=True)
+            procs.append((subprocess.Popen(flags), flags))
             objs.append(obj)
+        for proc, flags in procs:
+            if proc.wait() != 0:
+                raise subprocess.CalledProcessError(proc.returncode, flags)
         _run([HIPCC, "-shared", "-fPIC", "-pthread", "-o", LIB] + objs + ["-lamdhip64"], verbose)
         for o in objs:
             os.remove(o)

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -14,6 +15,7 @@
 #include <vector>
 
 #include "hnsw_build.h"
+#include "flat_kernels.h"
 #include "search_kernels.h"
 
 using alaya_amd::HostGraph;
@@ -107,6 +109,10 @@ struct alaya_index {
   int sq8_order = 2;
   uint32_t code_stride = 0;
   DevBuf codes, sq_min, sq_max, rr_q_buf;
+  // flat path
+  DevBuf norms, cand_d, cand_i, flag_buf, iota;
+  bool norms_ready = false;
+  float max_norm = 0.f;
   // scratch
   DevBuf work, overflow, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
   uint32_t hash_log2_override = 0;
@@ -204,6 +210,55 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   p.work_counter = ix->work.as<uint32_t>();
   hip_check(hipMemsetAsync(p.work_counter, 0, 4, stream), "hipMemsetAsync");
   hip_check(alaya_amd::launch_search(p, grid, lds, stream), "search launch");
+}
+
+void ensure_norms(alaya_index *ix, hipStream_t stream) {
+  if (ix->norms_ready) return;
+  ix->norms.reserve(std::max<uint64_t>(ix->n, 1) * 4);
+  hip_check(alaya_amd::launch_row_norms(ix->base.as<float>(), ix->n, ix->stride, ix->norms.as<float>(), stream),
+            "row norms");
+  std::vector<float> h(ix->n);
+  hip_check(hipMemcpyAsync(h.data(), ix->norms.ptr, ix->n * 4, hipMemcpyDeviceToHost, stream), "D2H");
+  hip_check(hipStreamSynchronize(stream), "norms");
+  float mx = 0.f;
+  for (float v : h) mx = std::max(mx, v);
+  ix->max_norm = std::sqrt(mx) * 1.0001f;
+  ix->norms_ready = true;
+}
+
+alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t *d_ids,
+                                  float *d_dists, uint32_t *d_flags, int *blocks) {
+  if (!ix->base.ptr) throw ArgError("index has no base vectors");
+  if (ix->metric != ALAYA_METRIC_L2) throw ArgError("the flat MFMA path supports the L2 metric");
+  if (alaya_amd::flat_scan_lds(ix->stride) == 0) throw ArgError("the flat MFMA path supports dim <= 224");
+  if (k == 0 || k > static_cast<uint32_t>(alaya_amd::flat_shortlist()) - 8) throw ArgError("flat search needs 1 <= k <= 24");
+  alaya_amd::FlatParams p{};
+  p.base = ix->base.as<float>();
+  p.n = ix->n;
+  p.dim = ix->dim;
+  p.stride = ix->stride;
+  p.norms = ix->norms.as<float>();
+  p.max_norm = ix->max_norm;
+  p.queries = d_q;
+  p.nq = nq;
+  p.q_stride = ix->dim;
+  const int nqg = static_cast<int>((nq + 127) / 128);
+  int chunks = (ix->num_cus + nqg - 1) / nqg;
+  chunks = std::max(8, (chunks + 7) / 8 * 8);
+  const uint64_t max_chunks = std::max<uint64_t>(8, (ix->n / 64) / 8 * 8);
+  chunks = static_cast<int>(std::min<uint64_t>(chunks, max_chunks));
+  p.n_chunks = chunks;
+  const size_t cand = static_cast<size_t>(chunks) * nq * alaya_amd::flat_shortlist();
+  ix->cand_d.reserve(cand * 4);
+  ix->cand_i.reserve(cand * 4);
+  p.cand_d = ix->cand_d.as<float>();
+  p.cand_i = ix->cand_i.as<uint32_t>();
+  p.k = k;
+  p.out_ids = d_ids;
+  p.out_dists = d_dists;
+  p.flags = d_flags;
+  *blocks = nqg * chunks;
+  return p;
 }
 
 }  // namespace
@@ -373,6 +428,7 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     ix->stride = stride;
     ix->metric = metric;
     ix->overflow.release();
+    ix->norms_ready = false;
   });
 }
 
@@ -622,6 +678,84 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
     if (counters)
       hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");
     hip_check(hipStreamSynchronize(ix->stream), "sq8 search");
+  });
+}
+
+// ---- flat exact k-NN (MFMA shortlist + exact rescoring) ---------------------------------------
+int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
+                                   uint32_t *d_ids, float *d_dists, uint32_t *d_flags, void *stream) {
+  return guarded([&] {
+    if (!ix || (nq && (!d_queries || !d_ids))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (nq == 0) return;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ensure_norms(ix, s);
+    int blocks = 0;
+    alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
+    hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
+    hip_check(alaya_amd::launch_flat_merge(p, s), "flat merge");
+  });
+}
+
+int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
+                            uint32_t *ids, float *dists, uint32_t *n_recomputed) {
+  return guarded([&] {
+    if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (n_recomputed) *n_recomputed = 0;
+    if (nq == 0) return;
+    ensure_norms(ix, ix->stream);
+    ix->q_buf.reserve(nq * ix->dim * 4);
+    ix->id_buf.reserve(nq * k * 4);
+    ix->dist_buf.reserve(nq * k * 4);
+    ix->flag_buf.reserve(nq * 4);
+    hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
+    int blocks = 0;
+    alaya_amd::FlatParams p = flat_params(ix, ix->q_buf.as<float>(), nq, k, ix->id_buf.as<uint32_t>(),
+                                          ix->dist_buf.as<float>(), ix->flag_buf.as<uint32_t>(), &blocks);
+    hip_check(alaya_amd::launch_flat_scan(p, blocks, ix->stream), "flat scan");
+    hip_check(alaya_amd::launch_flat_merge(p, ix->stream), "flat merge");
+    std::vector<uint32_t> flags(nq);
+    hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    std::vector<float> dv(nq * k);
+    hip_check(hipMemcpyAsync(dv.data(), ix->dist_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipMemcpyAsync(flags.data(), ix->flag_buf.ptr, nq * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipStreamSynchronize(ix->stream), "flat search");
+    // queries whose shortlist bound did not hold: exhaustive exact distances on the device
+    uint32_t redo = 0;
+    for (uint64_t q = 0; q < nq; ++q) {
+      if (!flags[q]) continue;
+      ++redo;
+      if (!ix->iota.ptr || ix->iota.bytes < ix->n * 4) {
+        std::vector<uint32_t> io(ix->n);
+        for (uint64_t i = 0; i < ix->n; ++i) io[i] = static_cast<uint32_t>(i);
+        ix->iota.reserve(ix->n * 4);
+        hip_check(hipMemcpy(ix->iota.ptr, io.data(), ix->n * 4, hipMemcpyHostToDevice), "H2D");
+      }
+      ix->dout_buf.reserve(ix->n * 4);
+      SearchParams sp = base_params(ix);
+      sp.queries = ix->q_buf.as<float>() + q * ix->dim;
+      sp.q_stride = ix->dim;
+      hip_check(alaya_amd::launch_row_distances(sp, ix->iota.as<uint32_t>(), static_cast<uint32_t>(ix->n), 1,
+                                                ix->dout_buf.as<float>(), ix->stream), "exhaustive");
+      std::vector<float> all(ix->n);
+      hip_check(hipMemcpyAsync(all.data(), ix->dout_buf.ptr, ix->n * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+      hip_check(hipStreamSynchronize(ix->stream), "exhaustive");
+      std::vector<uint32_t> order(ix->n);
+      for (uint64_t i = 0; i < ix->n; ++i) order[i] = static_cast<uint32_t>(i);
+      const uint64_t kk = std::min<uint64_t>(k, ix->n);
+      std::partial_sort(order.begin(), order.begin() + kk, order.end(), [&](uint32_t a, uint32_t b) {
+        return all[a] < all[b] || (all[a] == all[b] && a < b);
+      });
+      for (uint64_t j = 0; j < k; ++j) {
+        ids[q * k + j] = j < kk ? order[j] : 0u;
+        dv[q * k + j] = j < kk ? all[order[j]] : 0.f;
+      }
+    }
+    if (dists) std::memcpy(dists, dv.data(), nq * k * 4);
+    if (n_recomputed) *n_recomputed = redo;
   });
 }
 

@@ -1,0 +1,35 @@
+// Flat (exhaustive) exact k-NN: MFMA shortlist + exact rescoring (flat_kernels.hip).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace alaya_amd {
+
+struct FlatParams {
+  const float *base;   // n x stride f32 rows (zero padded)
+  uint64_t n;
+  uint32_t dim;
+  uint32_t stride;     // multiple of 32, at most 256 for the MFMA scan
+  const float *norms;  // |b|^2 per row
+  float max_norm;      // max |b|
+  const float *queries;
+  uint64_t nq;
+  uint32_t q_stride;
+  int n_chunks;        // base chunks (multiple of 8)
+  float *cand_d;       // n_chunks x nq x shortlist approximate distances
+  uint32_t *cand_i;
+  uint32_t k;
+  uint32_t *out_ids;   // nq x k
+  float *out_dists;    // nq x k, nullable
+  uint32_t *flags;     // nq: 1 = shortlist bound not proven, recompute exhaustively
+};
+
+int flat_shortlist();
+size_t flat_scan_lds(uint32_t stride);
+hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, float *norms, hipStream_t s);
+hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s);
+hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s);
+
+}  // namespace alaya_amd

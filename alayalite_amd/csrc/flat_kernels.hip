@@ -1,0 +1,413 @@
+// Flat (brute-force) exact k-NN on gfx950: the f32-MFMA contraction -2 Q B^T + |b|^2 with a fused
+// per-query shortlist, then an exact rescoring pass.  The reference has no FLAT index
+// (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); its brute-force analogues are
+// find_exact_gt (include/utils/evaluate.hpp:29-62) and calc_gt (python/src/alayalite/utils.py:99-105).
+// Result contract: the k nearest rows by the reference metric function (l2_sqr_avx2 order, the same
+// device function as the graph search) with ties broken by id, plus a per-query flag that is set
+// when the shortlist cannot be proven to contain them (error bound below) -- the host then
+// recomputes that query exhaustively.
+//
+// flat_scan_kernel: 256 threads = 4 waves, 128 queries per block (32 per wave), one base chunk per
+// block.  Each wave holds its 32 queries as MFMA A fragments in VGPRs: lane l owns query (l & 31),
+// k in [h*K/2, (h+1)*K/2) with h = l >> 5 (the k order is free -- the GEMM only ranks candidates).
+// Base rows stream through a double-buffered LDS tile of 32 rows (row pitch K+4 floats, so the 16
+// lanes of a ds_read_b128 group hit distinct bank quads).  Per 32-row tile a wave issues K/2
+// v_mfma_f32_32x32x2f32 into one 32x32 accumulator (C[query][row]: row = lane & 31, query =
+// (r&3) + 8(r>>2) + 4h for accumulator register r).  Approximate distance a = |b|^2 - 2 C.
+// Candidates below the query's running threshold are appended to a per-query LDS buffer; a wave
+// merge (rank selection over list + buffer) keeps the 32 smallest and lowers the threshold.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "flat_kernels.h"
+
+namespace alaya_amd {
+namespace {
+
+constexpr int kL = 32;       // shortlist per (query, chunk)
+constexpr int kBuf = 64;     // candidate buffer per query
+constexpr int kTile = 32;    // base rows per LDS tile
+constexpr int kPad = 4;      // LDS row pitch padding (floats)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// (d, tie) total order used by every selection below: smaller distance first, then smaller tie key
+__device__ __forceinline__ bool before(float da, uint32_t ta, float db, uint32_t tb) {
+  return da < db || (da == db && ta < tb);
+}
+
+// Merge list (kL entries) and buffer (cnt <= kBuf entries) of one query into the kL smallest.
+// Wave-wide.  ld/li: list; bd/bi: buffer.  Returns the new threshold (max kept distance).
+__device__ float merge_list(float *ld, uint32_t *li, float *bd, uint32_t *bi, int cnt) {
+  const int lane = lane_id();
+  const int total = kL + cnt;
+  // element e: e < kL from the list, else buffer[e - kL]; tie key = row id
+  float d0 = FLT_MAX, d1 = FLT_MAX;
+  uint32_t i0 = 0xffffffffu, i1 = 0xffffffffu;
+  if (lane < total) {
+    d0 = lane < kL ? ld[lane] : bd[lane - kL];
+    i0 = lane < kL ? li[lane] : bi[lane - kL];
+  }
+  if (lane + 64 < total) {
+    d1 = bd[lane + 64 - kL];
+    i1 = bi[lane + 64 - kL];
+  }
+  uint32_t r0 = 0, r1 = 0;
+  for (int f = 0; f < total; ++f) {
+    const float df = f < 64 ? __shfl(d0, f) : __shfl(d1, f - 64);
+    const uint32_t tf = f < 64 ? __shfl(i0, f) : __shfl(i1, f - 64);
+    r0 += (before(df, tf, d0, i0) || (df == d0 && tf == i0 && f < lane)) ? 1u : 0u;
+    r1 += (before(df, tf, d1, i1) || (df == d1 && tf == i1 && f < lane + 64)) ? 1u : 0u;
+  }
+  wave_fence();
+  if (lane < total && r0 < kL) {
+    ld[r0] = d0;
+    li[r0] = i0;
+  }
+  if (lane + 64 < total && r1 < kL) {
+    ld[r1] = d1;
+    li[r1] = i1;
+  }
+  wave_fence();
+  return ld[kL - 1];  // ranks 0..kL-1 were all written: this is the kL-th smallest
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
+  static_assert(K % 8 == 0 && K <= 256, "K must be a multiple of 8, at most 256");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int kPitch = K + kPad;
+  float *tile = reinterpret_cast<float *>(smem);                       // 2 x kTile x kPitch
+  float *nrm = tile + 2 * kTile * kPitch;                               // 2 x kTile
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  unsigned char *wbase = smem + (2 * kTile * kPitch + 2 * kTile) * 4 + wave * 32 * (kL + kBuf) * 8 + wave * 32 * 4;
+  float *ld = reinterpret_cast<float *>(wbase);                 // 32 queries x kL
+  uint32_t *li = reinterpret_cast<uint32_t *>(ld + 32 * kL);
+  float *bd = reinterpret_cast<float *>(li + 32 * kL);          // 32 queries x kBuf
+  uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kBuf);
+  int *cnt = reinterpret_cast<int *>(bi + 32 * kBuf);           // 32 counters
+
+  // XCD-aware block -> (query group, chunk): the query groups of one chunk share an XCD label.
+  const int nqg = static_cast<int>((p.nq + 127) / 128);
+  const int b = blockIdx.x;
+  const int qg = (b / 8) % nqg;
+  const int chunk = (b % 8) + 8 * (b / (8 * nqg));
+  if (chunk >= p.n_chunks) return;
+  const uint64_t rows_per_chunk = (p.n + p.n_chunks - 1) / p.n_chunks;
+  const uint64_t r0 = chunk * rows_per_chunk;
+  const uint64_t r1 = min(p.n, r0 + rows_per_chunk);
+
+  // A fragments: query q0 + col, k in [h*K/2, h*K/2 + K/2)
+  const uint64_t q0 = static_cast<uint64_t>(qg) * 128 + wave * 32;
+  float a[K / 2];
+  {
+    const uint64_t qi = q0 + col;
+    const float *qp = p.queries + qi * p.q_stride + h * (K / 2);
+#pragma unroll
+    for (int s = 0; s < K / 2; s += 4) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qi < p.nq) v = *reinterpret_cast<const float4 *>(qp + s);
+      a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
+    }
+  }
+  for (int e = lane; e < 32 * kL; e += 64) {
+    ld[e] = FLT_MAX;
+    li[e] = 0xffffffffu;
+  }
+  if (lane < 32) cnt[lane] = 0;
+  float tau[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tau[r] = FLT_MAX;
+
+  // cooperative tile load: 32 rows x K floats, 256 threads, float4 each
+  constexpr int kVecPerRow = K / 4;
+  constexpr int kVecs = kTile * kVecPerRow;
+  constexpr int kPerThread = (kVecs + 255) / 256;
+  auto load_tile = [&](uint64_t row0, float4 (&reg)[kPerThread], float (&nr)[1]) {
+#pragma unroll
+    for (int v = 0; v < kPerThread; ++v) {
+      const int idx = threadIdx.x + v * 256;
+      reg[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < kVecs) {
+        const uint64_t row = row0 + idx / kVecPerRow;
+        if (row < r1) reg[v] = *reinterpret_cast<const float4 *>(p.base + row * p.stride + (idx % kVecPerRow) * 4);
+      }
+    }
+    nr[0] = 0.f;
+    if (threadIdx.x < kTile) {
+      const uint64_t row = row0 + threadIdx.x;
+      nr[0] = row < r1 ? p.norms[row] : FLT_MAX;
+    }
+  };
+  auto store_tile = [&](int buf, const float4 (&reg)[kPerThread], const float (&nr)[1]) {
+    float *t = tile + buf * kTile * kPitch;
+#pragma unroll
+    for (int v = 0; v < kPerThread; ++v) {
+      const int idx = threadIdx.x + v * 256;
+      if (idx < kVecs) *reinterpret_cast<float4 *>(t + (idx / kVecPerRow) * kPitch + (idx % kVecPerRow) * 4) = reg[v];
+    }
+    if (threadIdx.x < kTile) nrm[buf * kTile + threadIdx.x] = nr[0];
+  };
+
+  float4 stage[kPerThread];
+  float stage_n[1];
+  load_tile(r0, stage, stage_n);
+  store_tile(0, stage, stage_n);
+  __syncthreads();
+  int buf = 0;
+  for (uint64_t row0 = r0; row0 < r1; row0 += kTile) {
+    const bool more = row0 + kTile < r1;
+    if (more) load_tile(row0 + kTile, stage, stage_n);  // next tile in flight during the MFMAs
+    const float *t = tile + buf * kTile * kPitch + col * kPitch + h * (K / 2);
+    f32x16 c = {};
+#pragma unroll
+    for (int s = 0; s < K / 2; s += 4) {
+      const float4 bv = *reinterpret_cast<const float4 *>(t + s);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bv.x, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 1], bv.y, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 2], bv.z, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 3], bv.w, c, 0, 0, 0);
+    }
+    const float bn = nrm[buf * kTile + col];
+    const uint32_t rid = static_cast<uint32_t>(row0 + col);
+    // append candidates below each query's threshold
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
+      const float dv = fmaf(-2.0f, c[r], bn);
+      const bool pass = dv < tau[r] && row0 + col < r1;
+      const uint64_t mk = __ballot(pass);
+      const uint32_t half_mask = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
+      if (half_mask) {
+        const int base_cnt = cnt[qloc];
+        const int pos = base_cnt + __popc(half_mask & ((1u << col) - 1u));
+        if (pass) {
+          bd[qloc * kBuf + pos] = dv;
+          bi[qloc * kBuf + pos] = rid;
+        }
+      }
+      wave_fence();
+      if (col == 0 && half_mask) cnt[qloc] += __popc(half_mask);
+      wave_fence();
+    }
+    // merge queries whose buffer could overflow on the next tile
+    for (int qloc = 0; qloc < 32; ++qloc) {
+      const int cq = cnt[qloc];
+      if (cq > kBuf - kTile || (!more && cq > 0)) {
+        const float th = merge_list(ld + qloc * kL, li + qloc * kL, bd + qloc * kBuf, bi + qloc * kBuf, cq);
+        if (lane == 0) cnt[qloc] = 0;
+        wave_fence();
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((r & 3) + 8 * (r >> 2) + 4 * h == qloc) tau[r] = th;
+      }
+    }
+    if (more) {
+      store_tile(buf ^ 1, stage, stage_n);
+      buf ^= 1;
+    }
+    __syncthreads();
+  }
+  // write the per-(chunk, query) shortlist
+  for (int qloc = 0; qloc < 32; ++qloc) {
+    const uint64_t qi = q0 + qloc;
+    if (qi >= p.nq) break;
+    if (lane < kL) {
+      const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + lane;
+      p.cand_d[o] = ld[qloc * kL + lane];
+      p.cand_i[o] = li[qloc * kL + lane];
+    }
+  }
+}
+
+// Exact rescoring (l2_sqr_avx2 order, 8 lanes per row) of one query's shortlist.
+__device__ float exact_l2(const FlatParams &p, const float *q, uint32_t id, int m) {
+  const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
+  const int T = static_cast<int>(p.dim >> 5);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float4 x = *reinterpret_cast<const float4 *>(q + 32 * t + 4 * m);
+    const float4 y = *reinterpret_cast<const float4 *>(row + 32 * t + 4 * m);
+    const float d0 = x.x - y.x, d1 = x.y - y.y, d2 = x.z - y.z, d3 = x.w - y.w;
+    a0 = fmaf(d0, d0, a0); a1 = fmaf(d1, d1, a1); a2 = fmaf(d2, d2, a2); a3 = fmaf(d3, d3, a3);
+  }
+  const int nb8 = (static_cast<int>(p.dim) - 32 * T) >> 3;
+  if (m < 2) {
+    for (int bb = 0; bb < nb8; ++bb) {
+      const float4 x = *reinterpret_cast<const float4 *>(q + 32 * T + 8 * bb + 4 * m);
+      const float4 y = *reinterpret_cast<const float4 *>(row + 32 * T + 8 * bb + 4 * m);
+      const float d0 = x.x - y.x, d1 = x.y - y.y, d2 = x.z - y.z, d3 = x.w - y.w;
+      a0 = fmaf(d0, d0, a0); a1 = fmaf(d1, d1, a1); a2 = fmaf(d2, d2, a2); a3 = fmaf(d3, d3, a3);
+    }
+  }
+  a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
+  a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+  const float s0 = a0 + __shfl_xor(a0, 1), s1 = a1 + __shfl_xor(a1, 1);
+  const float s2 = a2 + __shfl_xor(a2, 1), s3 = a3 + __shfl_xor(a3, 1);
+  float res = (s0 + s1) + (s2 + s3);
+  for (int e = 32 * T + 8 * nb8; e < static_cast<int>(p.dim); ++e) {
+    const float d = q[e] - row[e];
+    res = fmaf(d, d, res);
+  }
+  return res;
+}
+
+// One wave per query: merge the chunk shortlists (approximate distances), rescore the best kL
+// exactly, sort by (exact distance, id), emit k, flag the query if the bound does not hold.
+__global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float *q = reinterpret_cast<float *>(smem);
+  float *ld = q + p.stride;
+  uint32_t *li = reinterpret_cast<uint32_t *>(ld + kL);
+  float *bd = reinterpret_cast<float *>(li + kL);
+  uint32_t *bi = reinterpret_cast<uint32_t *>(bd + kBuf);
+  float *ed = reinterpret_cast<float *>(bi + kBuf);
+  const int lane = lane_id();
+  for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
+    const float *qs = p.queries + qi * p.q_stride;
+    float qn = 0.f;
+    for (uint32_t e = lane; e < p.stride; e += 64) {
+      const float v = e < p.dim ? qs[e] : 0.f;
+      q[e] = v;
+      qn = fmaf(v, v, qn);
+    }
+    for (int off = 32; off > 0; off >>= 1) qn += __shfl_xor(qn, off);
+    if (lane < kL) {
+      ld[lane] = FLT_MAX;
+      li[lane] = 0xffffffffu;
+    }
+    wave_fence();
+    // chunk shortlists, 64 candidates at a time
+    const uint64_t total = static_cast<uint64_t>(p.n_chunks) * kL;
+    for (uint64_t c0 = 0; c0 < total; c0 += kBuf) {
+      const uint64_t e = c0 + lane;
+      const int chunk = static_cast<int>(e / kL), slot = static_cast<int>(e % kL);
+      const int cnt = static_cast<int>(min<uint64_t>(kBuf, total - c0));
+      if (lane < cnt) {
+        const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + slot;
+        bd[lane] = p.cand_d[o];
+        bi[lane] = p.cand_i[o];
+      }
+      wave_fence();
+      merge_list(ld, li, bd, bi, cnt);
+    }
+    const float cutoff = ld[kL - 1];  // every row outside the shortlist has approx >= cutoff
+    // exact distances of the shortlist (8 lanes per row, 8 rows per pass)
+    const int g = lane >> 3, m = lane & 7;
+    for (int base = 0; base < kL; base += 8) {
+      const uint32_t id = li[base + g];
+      const bool ok = id != 0xffffffffu;
+      const float d = exact_l2(p, q, ok ? id : 0u, m);
+      if (m == 0) ed[base + g] = ok ? d : FLT_MAX;
+    }
+    wave_fence();
+    // rank by (exact distance, id)
+    float dv = FLT_MAX;
+    uint32_t iv = 0xffffffffu;
+    if (lane < kL) {
+      dv = ed[lane];
+      iv = li[lane];
+    }
+    uint32_t rank = 0;
+    for (int f = 0; f < kL; ++f) {
+      const float df = __shfl(dv, f);
+      const uint32_t tf = __shfl(iv, f);
+      rank += before(df, tf, dv, iv) ? 1u : 0u;
+    }
+    if (lane < kL && rank < p.k) {
+      p.out_ids[qi * p.k + rank] = iv;
+      if (p.out_dists) p.out_dists[qi * p.k + rank] = dv;
+    }
+    // bound: rows outside the shortlist have true distance >= cutoff + |q|^2 - eps, where the
+    // shortlist GEMM error is <= gamma_K * (|q|^2 + max|b|^2 + 2|q| max|b|); the exact f32 value of
+    // the k-th result has relative error <= gamma_K.  gamma_K = 2 K u with u = 2^-24 (conservative).
+    float kth_d = 0.f;
+    {
+      const uint64_t mk = __ballot(lane < kL && rank == p.k - 1);
+      kth_d = mk ? __shfl(dv, __ffsll(static_cast<unsigned long long>(mk)) - 1) : FLT_MAX;
+    }
+    const float gam = 2.0f * static_cast<float>(p.stride) * 5.9604645e-8f;
+    const float qnorm = sqrtf(qn);
+    const float bmax = p.max_norm;
+    const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax);
+    const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
+    if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
+    wave_fence();
+  }
+}
+
+__global__ void row_norms_kernel(const float *base, uint64_t n, uint32_t stride, float *norms) {
+  const uint64_t row = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  float s = 0.f;
+  for (uint32_t e = lane; e < stride; e += 64) {
+    const float v = base[row * stride + e];
+    s = fmaf(v, v, s);
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) norms[row] = s;
+}
+
+template <int K>
+size_t scan_lds() {
+  return (2 * kTile * (K + kPad) + 2 * kTile) * 4 + 4 * (32 * (kL + kBuf) * 8 + 32 * 4);
+}
+
+}  // namespace
+
+int flat_shortlist() { return kL; }
+
+hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, float *norms, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(row_norms_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0, s, base, n, stride, norms);
+  return hipGetLastError();
+}
+
+size_t flat_scan_lds(uint32_t stride) {
+  switch (stride) {
+    case 32: return scan_lds<32>();
+    case 64: return scan_lds<64>();
+    case 96: return scan_lds<96>();
+    case 128: return scan_lds<128>();
+    case 160: return scan_lds<160>();
+    case 192: return scan_lds<192>();
+    case 224: return scan_lds<224>();
+    default: return 0;  // 256: double-buffered 32-row tile + shortlists exceed 160 KB of LDS
+  }
+}
+
+hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
+  const size_t lds = flat_scan_lds(p.stride);
+  if (lds == 0) return hipErrorInvalidValue;
+#define ALAYA_FLAT(K)                                                                          \
+  case K:                                                                                      \
+    hipLaunchKernelGGL(flat_scan_kernel<K>, dim3(blocks), dim3(256), lds, s, p);               \
+    break;
+  switch (p.stride) {
+    ALAYA_FLAT(32) ALAYA_FLAT(64) ALAYA_FLAT(96) ALAYA_FLAT(128) ALAYA_FLAT(160) ALAYA_FLAT(192)
+    ALAYA_FLAT(224)
+    default: return hipErrorInvalidValue;
+  }
+#undef ALAYA_FLAT
+  return hipGetLastError();
+}
+
+hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s) {
+  const size_t lds = (static_cast<size_t>(p.stride) + 3 * kL + 2 * kBuf) * 4 + 64;
+  const int grid = static_cast<int>(p.nq < 4096 ? p.nq : 4096);
+  hipLaunchKernelGGL(flat_merge_kernel, dim3(grid), dim3(64), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace alaya_amd

@@ -668,6 +668,26 @@ class DeviceIndex {
                                        d.mutable_data(), c.mutable_data()));
     return py::make_tuple(ids, d, c);
   }
+  py::tuple flat_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k) {
+    const uint64_t nq = q.shape(0);
+    py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
+    py::array_t<float> d({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
+    uint32_t redo = 0;
+    const float *qp = q.data();
+    uint32_t *ip = ids.mutable_data();
+    float *dp = d.mutable_data();
+    {
+      py::gil_scoped_release nogil;
+      check(alaya_index_flat_search(ix_, qp, nq, k, ip, dp, &redo));
+    }
+    return py::make_tuple(ids, d, redo);
+  }
+  void flat_search_device(uintptr_t q, uint64_t nq, uint32_t k, uintptr_t ids, uintptr_t dists,
+                          uintptr_t flags, uintptr_t stream) {
+    check(alaya_index_flat_search_device(ix_, reinterpret_cast<const float *>(q), nq, k,
+                                         reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
+                                         reinterpret_cast<uint32_t *>(flags), reinterpret_cast<void *>(stream)));
+  }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
   py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
                            uint32_t ef) {
@@ -777,6 +797,8 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("search_device", &DeviceIndex::search_device)
       .def("distances", &DeviceIndex::distances)
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
+      .def("flat_search", &DeviceIndex::flat_search, py::arg("queries"), py::arg("k"))
+      .def("flat_search_device", &DeviceIndex::flat_search_device)
       .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)
       .def("search_sq8", &DeviceIndex::search_sq8, py::arg("queries"), py::arg("k"), py::arg("ef"),
            py::arg("rerank") = true, py::arg("rerank_queries") = py::none())

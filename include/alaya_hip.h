@@ -112,6 +112,17 @@ int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint3
 int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
                                  uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
                                  float *dists, uint32_t *counters);
+/* ---- flat (exhaustive) exact k-NN, L2, dim <= 224, k <= 24 --------------------------------------
+ * No reference implementation (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); the
+ * analogue is find_exact_gt (include/utils/evaluate.hpp:29-62).  An f32-MFMA pass ranks every row
+ * by |b|^2 - 2 q.b and keeps a shortlist; the shortlist is rescored with the exact device metric
+ * (l2_sqr_avx2 order) and sorted by (distance, id).  A query whose shortlist cannot be proven to
+ * hold the exact top-k (error bound in flat_kernels.hip) is flagged; the host API recomputes it
+ * exhaustively and reports how many it did. */
+int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
+                            uint32_t *ids, float *dists, uint32_t *n_recomputed);
+int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
+                                   uint32_t *d_ids, float *d_dists, uint32_t *d_flags, void *stream);
 /* Tuning / introspection: LDS visited-table size (log2 slots; 0 = automatic). */
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots);
 int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,

@@ -1,0 +1,67 @@
+"""Flat exact k-NN (BASELINE config 2's path; no reference implementation -- IndexType::FLAT is
+enum-only).  Contract: the k smallest rows by the reference metric function (the l2_sqr_avx2-order
+device distance, bit-identical to the CPU restatement) with ties broken by id."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _exact(orc, base, q, k):
+    lib = orc.lib()
+    out_i = np.zeros((len(q), k), np.uint32)
+    out_d = np.zeros((len(q), k), np.float32)
+    for a in range(len(q)):
+        qa = np.ascontiguousarray(q[a])
+        d = np.array([lib.orc_l2_f32(orc._ptr(qa), orc._ptr(base[i]), base.shape[1]) for i in range(len(base))],
+                     np.float32)
+        o = np.lexsort((np.arange(len(base)), d))[:k]
+        out_i[a], out_d[a] = o, d[o]
+    return out_i, out_d
+
+
+@pytest.mark.parametrize("n,d,nq", [(5000, 128, 37), (3000, 32, 130), (2500, 100, 9), (4000, 200, 64),
+                                    (2000, 224, 5), (777, 64, 300)])
+def test_flat_exact(native, orc, n, d, nq):
+    rng = np.random.default_rng(n + d)
+    base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
+    q = np.ascontiguousarray(rng.random((nq, d), dtype=np.float32))
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    ref_i, ref_d = _exact(orc, base, q, 10)
+    assert np.array_equal(ids, ref_i)
+    assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+
+
+def test_flat_rejects_unsupported(native):
+    dev = native.DeviceIndex(0)
+    dev.set_base(np.zeros((100, 300), np.float32), 0)
+    with pytest.raises(ValueError, match="dim <= 224"):
+        dev.flat_search(np.zeros((1, 300), np.float32), 10)
+
+
+def test_flat_ties_and_fallback(native, orc):
+    """Identical rows: every distance ties, so the shortlist bound cannot be proven -- the host
+    recomputes exhaustively and the answer is ids 0..k-1 (ties by id)."""
+    rng = np.random.default_rng(1)
+    row = rng.random(64, dtype=np.float32)
+    base = np.tile(row, (600, 1))
+    q = rng.random((3, 64), dtype=np.float32)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    assert redo == 3
+    assert (ids == np.arange(10, dtype=np.uint32)).all()
+
+
+def test_flat_duplicates_sift_like(native, orc):
+    rng = np.random.default_rng(2)
+    base = rng.integers(0, 4, (3000, 32)).astype(np.float32)  # many exact ties
+    q = rng.integers(0, 4, (20, 32)).astype(np.float32)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    ref_i, ref_d = _exact(orc, base, q, 10)
+    assert np.array_equal(ids, ref_i) and np.array_equal(dists, ref_d)
