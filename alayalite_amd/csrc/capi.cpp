@@ -682,6 +682,22 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
 }
 
 // ---- flat exact k-NN (MFMA shortlist + exact rescoring) ---------------------------------------
+int alaya_index_flat_diag(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k, int ablate,
+                          uint32_t *d_ids, float *d_dists, uint32_t *d_flags, uint32_t *d_merge_count,
+                          void *stream) {
+  return guarded([&] {
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ensure_norms(ix, s);
+    int blocks = 0;
+    alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
+    p.ablate = ablate;
+    p.merge_count = d_merge_count;
+    hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
+  });
+}
+
 int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
                                    uint32_t *d_ids, float *d_dists, uint32_t *d_flags, void *stream) {
   return guarded([&] {

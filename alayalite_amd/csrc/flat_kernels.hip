@@ -14,8 +14,10 @@
 // lanes of a ds_read_b128 group hit distinct bank quads).  Per 32-row tile a wave issues K/2
 // v_mfma_f32_32x32x2f32 into one 32x32 accumulator (C[query][row]: row = lane & 31, query =
 // (r&3) + 8(r>>2) + 4h for accumulator register r).  Approximate distance a = |b|^2 - 2 C.
-// Candidates below the query's running threshold are appended to a per-query LDS buffer; a wave
-// merge (rank selection over list + buffer) keeps the 32 smallest and lowers the threshold.
+// Candidates below the query's running threshold are appended to a per-query LDS buffer.  The
+// shortlists themselves live in registers laid out like the accumulator (register r, half h <->
+// query (r&3) + 8(r>>2) + 4h, entry = lane & 31), so a buffer is folded in by a 32-lane bitonic
+// sort + merge on ds_swizzle, without leaving the half-wave that owns the query.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -27,7 +29,7 @@ namespace alaya_amd {
 namespace {
 
 constexpr int kL = 32;       // shortlist per (query, chunk)
-constexpr int kBuf = 64;     // candidate buffer per query
+constexpr int kBuf = 96;     // candidate buffer per query
 constexpr int kTile = 32;    // base rows per LDS tile
 constexpr int kPad = 4;      // LDS row pitch padding (floats)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -44,40 +46,68 @@ __device__ __forceinline__ bool before(float da, uint32_t ta, float db, uint32_t
   return da < db || (da == db && ta < tb);
 }
 
-// Merge list (kL entries) and buffer (cnt <= kBuf entries) of one query into the kL smallest.
-// Wave-wide.  ld/li: list; bd/bi: buffer.  Returns the new threshold (max kept distance).
-__device__ float merge_list(float *ld, uint32_t *li, float *bd, uint32_t *bi, int cnt) {
-  const int lane = lane_id();
-  const int total = kL + cnt;
-  // element e: e < kL from the list, else buffer[e - kL]; tie key = row id
-  float d0 = FLT_MAX, d1 = FLT_MAX;
-  uint32_t i0 = 0xffffffffu, i1 = 0xffffffffu;
-  if (lane < total) {
-    d0 = lane < kL ? ld[lane] : bd[lane - kL];
-    i0 = lane < kL ? li[lane] : bi[lane - kL];
-  }
-  if (lane + 64 < total) {
-    d1 = bd[lane + 64 - kL];
-    i1 = bi[lane + 64 - kL];
-  }
-  uint32_t r0 = 0, r1 = 0;
-  for (int f = 0; f < total; ++f) {
-    const float df = f < 64 ? __shfl(d0, f) : __shfl(d1, f - 64);
-    const uint32_t tf = f < 64 ? __shfl(i0, f) : __shfl(i1, f - 64);
-    r0 += (before(df, tf, d0, i0) || (df == d0 && tf == i0 && f < lane)) ? 1u : 0u;
-    r1 += (before(df, tf, d1, i1) || (df == d1 && tf == i1 && f < lane + 64)) ? 1u : 0u;
-  }
-  wave_fence();
-  if (lane < total && r0 < kL) {
-    ld[r0] = d0;
-    li[r0] = i0;
-  }
-  if (lane + 64 < total && r1 < kL) {
-    ld[r1] = d1;
-    li[r1] = i1;
-  }
-  wave_fence();
-  return ld[kL - 1];  // ranks 0..kL-1 were all written: this is the kL-th smallest
+// ds_swizzle in bit mode stays inside each 32-lane half: source lane = ((l & 0x1f) | or) ^ xor.
+template <int kXor>
+__device__ __forceinline__ float swz_f(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1f | (kXor << 10)));
+}
+template <int kXor>
+__device__ __forceinline__ uint32_t swz_u(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x1f | (kXor << 10)));
+}
+__device__ __forceinline__ float lane31_of_half(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 31 << 5));
+}
+
+// One compare-exchange of a bitonic network over the 32 lanes of a half (block size K, distance J).
+template <int K, int J>
+__device__ __forceinline__ void cmpx(float &d, uint32_t &i, int col) {
+  const bool take_min = ((col & K) == 0) == ((col & J) == 0);
+  const float od = swz_f<J>(d);
+  const uint32_t oi = swz_u<J>(i);
+  // branch-free (d, id) comparison: short-circuit forms compile to nested exec-mask branches
+  const bool eq = od == d;
+  const bool o_first = (od < d) | (eq & (oi < i));
+  const bool m_first = (d < od) | (eq & (i < oi));
+  const bool sw = (take_min & o_first) | (!take_min & m_first);
+  d = sw ? od : d;
+  i = sw ? oi : i;
+}
+// bitonic sequence -> ascending
+__device__ __forceinline__ void bitonic_merge32(float &d, uint32_t &i, int col) {
+  cmpx<32, 16>(d, i, col);
+  cmpx<32, 8>(d, i, col);
+  cmpx<32, 4>(d, i, col);
+  cmpx<32, 2>(d, i, col);
+  cmpx<32, 1>(d, i, col);
+}
+__device__ __forceinline__ void bitonic_sort32(float &d, uint32_t &i, int col) {
+  cmpx<2, 1>(d, i, col);
+  cmpx<4, 2>(d, i, col);
+  cmpx<4, 1>(d, i, col);
+  cmpx<8, 4>(d, i, col);
+  cmpx<8, 2>(d, i, col);
+  cmpx<8, 1>(d, i, col);
+  cmpx<16, 8>(d, i, col);
+  cmpx<16, 4>(d, i, col);
+  cmpx<16, 2>(d, i, col);
+  cmpx<16, 1>(d, i, col);
+  bitonic_merge32(d, i, col);
+}
+// Fold 32 candidates (one per lane of the half, any order) into the ascending list (L, Li):
+// sort them, pair list[c] with candidate[31-c] (the min of each pair is a bitonic sequence holding
+// the 32 smallest of the union), re-sort.
+__device__ __forceinline__ void fold32_sorted(float &L, uint32_t &Li, float cd, uint32_t ci, int col) {
+  const float rd = swz_f<31>(cd);
+  const uint32_t ri = swz_u<31>(ci);
+  const bool take = (rd < L) | ((rd == L) & (ri < Li));
+  L = take ? rd : L;
+  Li = take ? ri : Li;
+  bitonic_merge32(L, Li, col);
+}
+__device__ __forceinline__ void fold32(float &L, uint32_t &Li, float cd, uint32_t ci, int col) {
+  bitonic_sort32(cd, ci, col);
+  fold32_sorted(L, Li, cd, ci, col);
 }
 
 template <int K>
@@ -90,12 +120,8 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
-  unsigned char *wbase = smem + (2 * kTile * kPitch + 2 * kTile) * 4 + wave * 32 * (kL + kBuf) * 8 + wave * 32 * 4;
-  float *ld = reinterpret_cast<float *>(wbase);                 // 32 queries x kL
-  uint32_t *li = reinterpret_cast<uint32_t *>(ld + 32 * kL);
-  float *bd = reinterpret_cast<float *>(li + 32 * kL);          // 32 queries x kBuf
+  float *bd = tile + 2 * kTile * kPitch + 2 * kTile + wave * 32 * kBuf * 2;  // 32 queries x kBuf
   uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kBuf);
-  int *cnt = reinterpret_cast<int *>(bi + 32 * kBuf);           // 32 counters
 
   // XCD-aware block -> (query group, chunk): the query groups of one chunk share an XCD label.
   const int nqg = static_cast<int>((p.nq + 127) / 128);
@@ -120,14 +146,19 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
     }
   }
-  for (int e = lane; e < 32 * kL; e += 64) {
-    ld[e] = FLT_MAX;
-    li[e] = 0xffffffffu;
-  }
-  if (lane < 32) cnt[lane] = 0;
-  float tau[16];
+  // Shortlists live in registers with the accumulator's layout: register r of half h holds the
+  // ascending list of query qloc(r, h), entry (lane & 31).  cnt[r] = buffered candidates of that
+  // query (uniform over the half), tau[r] = its current 32nd distance.
+  float ld[16], tau[16];
+  uint32_t li[16];
+  int cnt[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) tau[r] = FLT_MAX;
+  for (int r = 0; r < 16; ++r) {
+    ld[r] = FLT_MAX;
+    li[r] = 0xffffffffu;
+    tau[r] = FLT_MAX;
+    cnt[r] = 0;
+  }
 
   // cooperative tile load: 32 rows x K floats, 256 threads, float4 each
   constexpr int kVecPerRow = K / 4;
@@ -165,6 +196,8 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   store_tile(0, stage, stage_n);
   __syncthreads();
   int buf = 0;
+  uint64_t t_fold = 0, t_bar = 0, t_app = 0;
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
   for (uint64_t row0 = r0; row0 < r1; row0 += kTile) {
     const bool more = row0 + kTile < r1;
     if (more) load_tile(row0 + kTile, stage, stage_n);  // next tile in flight during the MFMAs
@@ -180,52 +213,130 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     }
     const float bn = nrm[buf * kTile + col];
     const uint32_t rid = static_cast<uint32_t>(row0 + col);
-    // append candidates below each query's threshold
+    const bool live = row0 + col < r1;
+    if (p.ablate == 1) {  // diagnostics: keep the accumulator live, skip the candidate path
+      float sink = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sink += c[r];
+      if (sink == -1.2345f) p.flags[0] = 7;
+      if (more) {
+        store_tile(buf ^ 1, stage, stage_n);
+        buf ^= 1;
+      }
+      __syncthreads();
+      continue;
+    }
+    // append candidates below each query's threshold (counts stay in registers)
+    const uint64_t ta = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t need = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
       const float dv = fmaf(-2.0f, c[r], bn);
-      const bool pass = dv < tau[r] && row0 + col < r1;
+      const bool pass = live && dv < tau[r];
       const uint64_t mk = __ballot(pass);
-      const uint32_t half_mask = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
-      if (half_mask) {
-        const int base_cnt = cnt[qloc];
-        const int pos = base_cnt + __popc(half_mask & ((1u << col) - 1u));
+      if (mk) {
+        const uint32_t hm = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
         if (pass) {
+          const int pos = cnt[r] + __popc(hm & ((1u << col) - 1u));
           bd[qloc * kBuf + pos] = dv;
           bi[qloc * kBuf + pos] = rid;
         }
+        cnt[r] += __popc(hm);
       }
-      wave_fence();
-      if (col == 0 && half_mask) cnt[qloc] += __popc(half_mask);
-      wave_fence();
+      if (__ballot(cnt[r] > kBuf - kTile || (!more && cnt[r] > 0))) need |= 1u << r;
     }
-    // merge queries whose buffer could overflow on the next tile
-    for (int qloc = 0; qloc < 32; ++qloc) {
-      const int cq = cnt[qloc];
-      if (cq > kBuf - kTile || (!more && cq > 0)) {
-        const float th = merge_list(ld + qloc * kL, li + qloc * kL, bd + qloc * kBuf, bi + qloc * kBuf, cq);
-        if (lane == 0) cnt[qloc] = 0;
-        wave_fence();
+    // Smoothing: besides the folds that are due, fold the fullest buffer once it holds a full
+    // batch.  One fold per wave per tile keeps the four waves' fold work level between barriers.
+    if (need == 0) {
+      int best = 0, best_r = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if ((r & 3) + 8 * (r >> 2) + 4 * h == qloc) tau[r] = th;
+      for (int r = 0; r < 16; ++r) {
+        const int m = max(__builtin_amdgcn_readlane(cnt[r], 0), __builtin_amdgcn_readlane(cnt[r], 32));
+        if (m > best) {
+          best = m;
+          best_r = r;
+        }
       }
+      if (best >= kTile) need = 1u << best_r;
     }
+    if (p.ablate == 2) {  // diagnostics: appends only, buffers dropped instead of folded
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (need & (1u << r)) cnt[r] = 0;
+      need = 0;
+    }
+    // Fold the buffers that could overflow on the next tile into their shortlists.  One copy of the
+    // fold body (a uniform loop over `need`, the register picked by value): unrolling it per
+    // register would put ~48 KB of code in the loop and thrash the instruction cache.
+    const uint64_t tf = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
+    t_app += tf - ta;
+    if (need) {
+      wave_fence();
+      do {
+        const int r = __builtin_ctz(need);
+        need &= need - 1;
+        float L = ld[0];
+        uint32_t Li = li[0];
+        int cr = cnt[0];
+#pragma unroll
+        for (int r2 = 1; r2 < 16; ++r2) {
+          if (r2 == r) {
+            L = ld[r2];
+            Li = li[r2];
+            cr = cnt[r2];
+          }
+        }
+        const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int cmax = max(__builtin_amdgcn_readlane(cr, 0), __builtin_amdgcn_readlane(cr, 32));
+        for (int b0 = 0; b0 < cmax; b0 += 32) {
+          float cd = FLT_MAX;
+          uint32_t ci = 0xffffffffu;
+          if (b0 + col < cr) {
+            cd = bd[qloc * kBuf + b0 + col];
+            ci = bi[qloc * kBuf + b0 + col];
+          }
+          fold32(L, Li, cd, ci, col);
+        }
+        const float th = lane31_of_half(L);
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) {
+          if (r2 == r) {
+            ld[r2] = L;
+            li[r2] = Li;
+            cnt[r2] = 0;
+            tau[r2] = th;
+          }
+        }
+        if (lane == 0 && p.merge_count) atomicAdd(p.merge_count + blockIdx.x, 1u);
+      } while (need);
+      wave_fence();
+    }
+    const uint64_t tb = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
+    t_fold += tb - tf;
     if (more) {
       store_tile(buf ^ 1, stage, stage_n);
       buf ^= 1;
     }
     __syncthreads();
+    if (p.merge_count) t_bar += __builtin_amdgcn_s_memtime() - tb;
+  }
+  if (p.merge_count && lane == 0) {
+    // diagnostics: per-wave cycle split (s_memtime ticks) after the per-block merge counters
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * 4 + wave) * 4;
+    st[0] = __builtin_amdgcn_s_memtime() - t_start;
+    st[1] = t_app;
+    st[2] = t_fold;
+    st[3] = t_bar;
   }
   // write the per-(chunk, query) shortlist
-  for (int qloc = 0; qloc < 32; ++qloc) {
-    const uint64_t qi = q0 + qloc;
-    if (qi >= p.nq) break;
-    if (lane < kL) {
-      const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + lane;
-      p.cand_d[o] = ld[qloc * kL + lane];
-      p.cand_i[o] = li[qloc * kL + lane];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (qi < p.nq) {
+      const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
+      p.cand_d[o] = ld[r];
+      p.cand_i[o] = li[r];
     }
   }
 }
@@ -269,10 +380,9 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
   float *q = reinterpret_cast<float *>(smem);
   float *ld = q + p.stride;
   uint32_t *li = reinterpret_cast<uint32_t *>(ld + kL);
-  float *bd = reinterpret_cast<float *>(li + kL);
-  uint32_t *bi = reinterpret_cast<uint32_t *>(bd + kBuf);
-  float *ed = reinterpret_cast<float *>(bi + kBuf);
+  float *ed = reinterpret_cast<float *>(li + kL);
   const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
   for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
     const float *qs = p.queries + qi * p.q_stride;
     float qn = 0.f;
@@ -282,25 +392,26 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
       qn = fmaf(v, v, qn);
     }
     for (int off = 32; off > 0; off >>= 1) qn += __shfl_xor(qn, off);
+    // chunk shortlists (each ascending): half h folds chunks h, h+2, ...; then the halves swap
+    float L = FLT_MAX;
+    uint32_t Li = 0xffffffffu;
+    for (int c0 = 0; c0 < p.n_chunks; c0 += 2) {
+      const int chunk = c0 + h;
+      float cd = FLT_MAX;
+      uint32_t ci = 0xffffffffu;
+      if (chunk < p.n_chunks) {
+        const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
+        cd = p.cand_d[o];
+        ci = p.cand_i[o];
+      }
+      fold32_sorted(L, Li, cd, ci, col);
+    }
+    fold32_sorted(L, Li, __shfl_xor(L, 32), __shfl_xor(Li, 32), col);
     if (lane < kL) {
-      ld[lane] = FLT_MAX;
-      li[lane] = 0xffffffffu;
+      ld[lane] = L;
+      li[lane] = Li;
     }
     wave_fence();
-    // chunk shortlists, 64 candidates at a time
-    const uint64_t total = static_cast<uint64_t>(p.n_chunks) * kL;
-    for (uint64_t c0 = 0; c0 < total; c0 += kBuf) {
-      const uint64_t e = c0 + lane;
-      const int chunk = static_cast<int>(e / kL), slot = static_cast<int>(e % kL);
-      const int cnt = static_cast<int>(min<uint64_t>(kBuf, total - c0));
-      if (lane < cnt) {
-        const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + slot;
-        bd[lane] = p.cand_d[o];
-        bi[lane] = p.cand_i[o];
-      }
-      wave_fence();
-      merge_list(ld, li, bd, bi, cnt);
-    }
     const float cutoff = ld[kL - 1];  // every row outside the shortlist has approx >= cutoff
     // exact distances of the shortlist (8 lanes per row, 8 rows per pass)
     const int g = lane >> 3, m = lane & 7;
@@ -361,7 +472,7 @@ __global__ void row_norms_kernel(const float *base, uint64_t n, uint32_t stride,
 
 template <int K>
 size_t scan_lds() {
-  return (2 * kTile * (K + kPad) + 2 * kTile) * 4 + 4 * (32 * (kL + kBuf) * 8 + 32 * 4);
+  return (2 * kTile * (K + kPad) + 2 * kTile) * 4 + 4 * (32 * kBuf * 8);
 }
 
 }  // namespace

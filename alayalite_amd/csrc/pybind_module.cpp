@@ -17,6 +17,9 @@
 #include <vector>
 
 #include "../../include/alaya_hip.h"
+
+extern "C" int alaya_index_flat_diag(alaya_index *, const float *, uint64_t, uint32_t, int, uint32_t *, float *,
+                                     uint32_t *, uint32_t *, void *);
 #include "host_distance.h"
 
 namespace py = pybind11;
@@ -688,6 +691,13 @@ class DeviceIndex {
                                          reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
                                          reinterpret_cast<uint32_t *>(flags), reinterpret_cast<void *>(stream)));
   }
+  void flat_diag(uintptr_t q, uint64_t nq, uint32_t k, int ablate, uintptr_t ids, uintptr_t dists,
+                 uintptr_t flags, uintptr_t mc, uintptr_t stream) {
+    check(alaya_index_flat_diag(ix_, reinterpret_cast<const float *>(q), nq, k, ablate,
+                                reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
+                                reinterpret_cast<uint32_t *>(flags), reinterpret_cast<uint32_t *>(mc),
+                                reinterpret_cast<void *>(stream)));
+  }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
   py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
                            uint32_t ef) {
@@ -799,6 +809,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
       .def("flat_search", &DeviceIndex::flat_search, py::arg("queries"), py::arg("k"))
       .def("flat_search_device", &DeviceIndex::flat_search_device)
+      .def("flat_diag", &DeviceIndex::flat_diag)
       .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)
       .def("search_sq8", &DeviceIndex::search_sq8, py::arg("queries"), py::arg("k"), py::arg("ef"),
            py::arg("rerank") = true, py::arg("rerank_queries") = py::none())
