@@ -160,7 +160,7 @@ uint32_t auto_hash_log2(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t 
 
 void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t ef,
                uint32_t *d_ids, float *d_dists, uint32_t *d_cnt, hipStream_t stream,
-               uint64_t *d_stamps = nullptr, bool sq8 = false) {
+               uint64_t *d_stamps = nullptr, bool sq8 = false, uint32_t fill_id = 0) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
   if (!ix->has_graph) throw ArgError("index has no graph");
   if (ef == 0) throw ArgError("ef must be >= 1");
@@ -186,6 +186,7 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   p.out_dists = d_dists;
   p.out_counters = d_cnt;
   p.stamps = d_stamps;
+  p.fill_id = fill_id;
   if (sq8) {
     if (!ix->has_sq8) throw ArgError("index has no SQ8 codes");
     p.sq8_order = ix->sq8_order;
@@ -641,16 +642,19 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
                                  float *dists, uint32_t *counters) {
   return guarded([&] {
     if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
+    if (rerank < 0 || rerank > 2) throw ArgError("rerank must be 0 (none), 1 (reference) or 2 (corrected)");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
     if (nq == 0 || k == 0) return;
+    // corrected rerank: the search hands over its whole ef pool (kEmpty past the pool)
+    const uint32_t ks = rerank == 2 ? ef : k;
     ix->q_buf.reserve(nq * ix->dim * 4);
-    ix->id_buf.reserve(nq * k * 4);
-    ix->dist_buf.reserve(nq * k * 4);
+    ix->id_buf.reserve(nq * ks * 4);
+    ix->dist_buf.reserve(nq * ks * 4);
     ix->cnt_buf.reserve(nq * 16);
     hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
-    do_search(ix, ix->q_buf.as<float>(), nq, k, ef, ix->id_buf.as<uint32_t>(), ix->dist_buf.as<float>(),
-              ix->cnt_buf.as<uint32_t>(), ix->stream, nullptr, true);
+    do_search(ix, ix->q_buf.as<float>(), nq, ks, ef, ix->id_buf.as<uint32_t>(), ix->dist_buf.as<float>(),
+              ix->cnt_buf.as<uint32_t>(), ix->stream, nullptr, true, rerank == 2 ? 0xffffffffu : 0u);
     uint32_t *final_ids = ix->id_buf.as<uint32_t>();
     float *final_d = ix->dist_buf.as<float>();
     if (rerank) {
@@ -667,8 +671,8 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
       p.queries = rq;
       p.nq = nq;
       p.q_stride = ix->dim;
-      alaya_amd::RerankParams r{ix->id_buf.as<uint32_t>(), k, ef, ix->dlist_buf.as<uint32_t>(),
-                                ix->dout_buf.as<float>()};
+      alaya_amd::RerankParams r{ix->id_buf.as<uint32_t>(), k, ef, ks, rerank == 2 ? 1 : 0,
+                                ix->dlist_buf.as<uint32_t>(), ix->dout_buf.as<float>()};
       hip_check(alaya_amd::launch_rerank(p, r, ix->stream), "rerank launch");
       final_ids = ix->dlist_buf.as<uint32_t>();
       final_d = ix->dout_buf.as<float>();

@@ -209,6 +209,12 @@ class PyIndexInterface {
     return out;
   }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
+  // SQ8 batch_search rerank: 1 = the reference's PyIndex::rerank (default), 2 = corrected (whole ef pool)
+  void set_rerank_mode(int m) {
+    if (m != 1 && m != 2) throw std::invalid_argument("rerank mode must be 1 (reference) or 2 (corrected)");
+    rerank_mode_ = m;
+  }
+  int rerank_mode() const { return rerank_mode_; }
   py::array device_distances(py::array queries, py::array_t<uint32_t> ids) {
     py::array q = prepare_queries(queries);
     py::array_t<uint32_t, py::array::c_style | py::array::forcecast> idc(ids);
@@ -298,7 +304,7 @@ class PyIndexInterface {
       const float *sq = raw_queries_.empty() ? rq : raw_queries_.data();
       // batch_search reranks (index.hpp:337-345); batch_search_with_distance does not and returns
       // an empty distance array for SQ spaces (index.hpp:391-418, get_topk_array of no rows).
-      const int rerank = want_dist ? 0 : 1;
+      const int rerank = want_dist ? 0 : rerank_mode_;
       {
         py::gil_scoped_release nogil;
         check(alaya_index_batch_search_sq8(ix_, sq, rq, nq, topk, ef, rerank, ids32.data(),
@@ -517,6 +523,7 @@ class PyIndexInterface {
   std::vector<float> rows_f32_;    // float rows uploaded to HBM
   std::vector<uint8_t> valid_;     // empty = all valid
   std::vector<uint32_t> last_counters_;
+  int rerank_mode_ = 1;
   std::vector<float> raw_queries_;   // SQ8 + COS: the un-normalised queries the SQ8 search encodes
   std::vector<uint8_t> sq_codes_;
   std::vector<float> sq_min_, sq_max_;
@@ -656,7 +663,7 @@ class DeviceIndex {
                               mn.data(), mx.data(), order));
   }
   py::tuple search_sq8(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
-                       uint32_t ef, bool rerank, py::object rerank_queries) {
+                       uint32_t ef, int rerank, py::object rerank_queries) {
     const uint64_t nq = q.shape(0);
     py::array_t<float, py::array::c_style | py::array::forcecast> rq;
     const float *rqp = nullptr;
@@ -667,7 +674,7 @@ class DeviceIndex {
     py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
     py::array_t<float> d({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
     py::array_t<uint32_t> c({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(4)});
-    check(alaya_index_batch_search_sq8(ix_, q.data(), rqp, nq, k, ef, rerank ? 1 : 0, ids.mutable_data(),
+    check(alaya_index_batch_search_sq8(ix_, q.data(), rqp, nq, k, ef, rerank, ids.mutable_data(),
                                        d.mutable_data(), c.mutable_data()));
     return py::make_tuple(ids, d, c);
   }
@@ -787,6 +794,8 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("get_data_dim", &PyIndexInterface::get_data_dim)
       .def("last_counters", &PyIndexInterface::last_counters)
       .def("set_hash_log2", &PyIndexInterface::set_hash_log2)
+      .def("set_rerank_mode", &PyIndexInterface::set_rerank_mode)
+      .def("rerank_mode", &PyIndexInterface::rerank_mode)
       .def("device_distances", &PyIndexInterface::device_distances)
       .def("graph_arrays", &PyIndexInterface::graph_arrays);
 
@@ -812,7 +821,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("flat_diag", &DeviceIndex::flat_diag)
       .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)
       .def("search_sq8", &DeviceIndex::search_sq8, py::arg("queries"), py::arg("k"), py::arg("ef"),
-           py::arg("rerank") = true, py::arg("rerank_queries") = py::none())
+           py::arg("rerank") = 1, py::arg("rerank_queries") = py::none())
       .def("profile_search", &DeviceIndex::profile_search)
       .def("device_bytes", &DeviceIndex::device_bytes);
   m.def("sq8_train", [](py::array_t<float, py::array::c_style | py::array::forcecast> data) {

@@ -37,6 +37,7 @@ struct SearchParams {
   uint32_t *out_ids;      // nq x k
   float *out_dists;       // nq x k (nullable)
   uint32_t *out_counters; // nq x 4 (n_dist, n_expand, n_dist_upper, n_hops_upper), nullable
+  uint32_t fill_id;       // id written for result slots past the pool (0 = reference behaviour)
   // scratch
   uint32_t *work_counter; // zeroed before each launch
   uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area
@@ -52,8 +53,10 @@ struct SearchParams {
 
 // PyIndex::rerank inputs (python/include/index.hpp:450-488).
 struct RerankParams {
-  const uint32_t *search_ids;  // nq x k ids written by the SQ8 search
+  const uint32_t *search_ids;  // nq x n_src ids written by the SQ8 search
   uint32_t k, ef;
+  uint32_t n_src;              // ids per query in search_ids (k, or ef in corrected mode)
+  int corrected;               // 0: reference (ef-k zero entries rescored), 1: the ef pool entries
   uint32_t *out_ids;           // nq x k
   float *out_dists;            // nq x k (nullable)
 };

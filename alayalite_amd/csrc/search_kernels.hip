@@ -479,7 +479,7 @@ __device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L) {
 // --------------------------------------------------------------------------------------------
 // kStamp: diagnostic build that accumulates s_memtime cycles per phase into p.stamps (nq x 8):
 // [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
-// [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] unused.
+// [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] prefetch hits.
 template <bool kIP, int kChunks, bool kStamp, int kSpace = 0>
 __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -639,13 +639,24 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
 
     // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
     stamp(0);
+    // Adjacency prefetch (no semantic effect): after a pop, the first unchecked entry is the next
+    // expansion unless the merge puts a closer candidate in front of it.  Its 128 B row is loaded
+    // into registers while this expansion runs and used only if the next pop returns that id.
+    uint32_t pred = kEmpty, pred_v = kEmpty;
     while (ps.cur < ps.size) {
       const uint32_t u = pool_pop(ps, L);
       ++n_expand;
       if (kStamp && vs.spilled) st[5]++;
       stamp(1);
-      const uint32_t *adj = p.l0 + static_cast<uint64_t>(u) * p.R;
-      uint32_t v = lane < static_cast<int>(p.R) ? adj[lane] : kEmpty;
+      uint32_t v;
+      if (u == pred) {
+        v = pred_v;
+        if (kStamp) st[7]++;
+      } else {
+        v = lane < static_cast<int>(p.R) ? p.l0[static_cast<uint64_t>(u) * p.R + lane] : kEmpty;
+      }
+      pred = ps.cur < ps.size ? (L.pi[ps.cur] & kIdMask) : kEmpty;
+      if (pred != kEmpty && lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(pred) * p.R + lane];
       const uint64_t endm = ballot(lane < static_cast<int>(p.R) && v == kEmpty);
       const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1 : static_cast<int>(p.R);
       bool act = lane < cnt;
@@ -678,7 +689,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
 
     // ---- results (ids[i] = pool.id(i), distances[i] = pool.dist(i)) --------------------------
     for (uint32_t i = lane; i < p.k; i += 64) {
-      uint32_t id = 0;
+      uint32_t id = p.fill_id;
       float d = 0.f;
       if (i < ps.size) {
         id = L.pi[i] & kIdMask;
@@ -730,25 +741,40 @@ __global__ void __launch_bounds__(64) row_distance_kernel(SearchParams p, const 
 // PyIndex::rerank (python/include/index.hpp:450-488) for SQ8 indexes, Linux batch path (:337-345):
 // res_pool[i] holds the k ids the search wrote plus ef-k zeros; all ef entries are rescored with
 // the raw-space QueryComputer (f32 rows, FLT_MAX for invalid rows) and the k smallest
-// pair<dist, id> are returned (id 0 can repeat -- reference behaviour).  One wave per query.
+// pair<dist, id> are returned (id 0 can repeat -- reference behaviour).  Corrected mode (SURVEY
+// A12 "corrected mode behind a flag"): the search hands over its whole ef pool (slots past the pool
+// hold kEmpty and are skipped), so every rescored entry is a real candidate.  One wave per query.
 template <bool kIP>
 __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams rp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float *q = reinterpret_cast<float *>(smem);
   uint32_t *cid = reinterpret_cast<uint32_t *>(smem + static_cast<size_t>(p.stride) * 4);
-  const uint32_t cap = rp.k + 1;
+  const uint32_t cap = max(rp.k, rp.n_src) + 1;
   float *cd = reinterpret_cast<float *>(cid + cap);
   uint32_t *cm = reinterpret_cast<uint32_t *>(cd + cap);
   const int lane = lane_id();
-  const uint32_t taken = min(rp.k, rp.ef);
-  const uint32_t zeros = rp.ef > rp.k ? rp.ef - rp.k : 0u;
+  const uint32_t taken = rp.corrected ? rp.n_src : min(rp.k, rp.ef);
+  const uint32_t zeros = (!rp.corrected && rp.ef > rp.k) ? rp.ef - rp.k : 0u;
   const uint32_t c = taken + (zeros ? 1u : 0u);
   for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
     const float *qsrc = p.queries + qi * p.q_stride;
     for (uint32_t e = lane; e < p.stride; e += 64) q[e] = e < p.dim ? qsrc[e] : 0.f;
-    for (uint32_t i = lane; i < c; i += 64) {
-      cid[i] = i < taken ? rp.search_ids[qi * rp.k + i] : 0u;
-      cm[i] = i < taken ? 1u : zeros;
+    uint32_t nv = 0;  // entries that will be emitted (with multiplicity)
+    for (uint32_t b = 0; b < c; b += 64) {
+      const uint32_t i = b + lane;
+      uint32_t id = 0, m = 0;
+      if (i < c) {
+        id = i < taken ? rp.search_ids[qi * rp.n_src + i] : 0u;
+        m = i < taken ? 1u : zeros;
+        if (id == kEmpty) {  // corrected mode: slot past the pool
+          id = 0u;
+          m = 0u;
+        }
+        cid[i] = id;
+        cm[i] = m;
+      }
+      for (int off = 32; off > 0; off >>= 1) m += __shfl_xor(m, off);
+      nv += m;
     }
     wave_sync();
     row_distances<kIP, 0>(p, q, cid, static_cast<int>(c), cd);
@@ -769,7 +795,7 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
         if (rp.out_dists) rp.out_dists[qi * rp.k + rank + m] = di;
       }
     }
-    for (uint32_t i = taken + zeros + lane; i < rp.k; i += 64) {  // ef < k: nothing left to pop
+    for (uint32_t i = nv + lane; i < rp.k; i += 64) {  // fewer candidates than k
       rp.out_ids[qi * rp.k + i] = 0u;
       if (rp.out_dists) rp.out_dists[qi * rp.k + i] = 0.f;
     }
@@ -784,7 +810,7 @@ size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool s
 }
 
 hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream) {
-  const size_t lds = static_cast<size_t>(p.stride) * 4 + 3 * (static_cast<size_t>(r.k) + 1) * 4 + 64;
+  const size_t lds = static_cast<size_t>(p.stride) * 4 + 3 * (static_cast<size_t>(std::max(r.k, r.n_src)) + 1) * 4 + 64;
   const int grid = static_cast<int>(std::min<uint64_t>(p.nq, 4096));
   if (p.ip) {
     hipLaunchKernelGGL(rerank_kernel<true>, dim3(grid), dim3(64), lds, stream, p, r);

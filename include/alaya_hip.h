@@ -107,8 +107,10 @@ int alaya_sq8_encode(const float *data, uint64_t n, uint32_t dim, const float *m
 int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint32_t dim,
                         const float *min_v, const float *max_v, int order);
 /* PyIndex::batch_search with SearchSpace = SQ8Space (index.hpp:289-346): graph search on the SQ8
- * codes (queries encoded in-kernel), then -- if rerank -- PyIndex::rerank on the f32 rows with
- * rerank_queries (NULL = queries) including its ef-k zero entries (index.hpp:450-488). */
+ * codes (queries encoded in-kernel), then a rerank on the f32 rows with rerank_queries (NULL =
+ * queries).  rerank: 0 = none (the SQ8 ids and distances), 1 = PyIndex::rerank as the reference
+ * runs it, including its ef-k zero entries (index.hpp:450-488), 2 = corrected: the whole ef pool
+ * is rescored (no id-0 duplicates); result slots beyond the candidates hold (0, 0.0). */
 int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
                                  uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
                                  float *dists, uint32_t *counters);

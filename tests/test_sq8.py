@@ -92,6 +92,38 @@ def test_sq8_rerank_quirk_on_device(native, orc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("metric", [0, 1])
+def test_sq8_corrected_rerank(native, orc, metric):
+    """rerank=2 (SURVEY A12 corrected mode): the whole ef pool of the SQ8 search is rescored with
+    the exact f32 metric and the k smallest (dist, id) come back -- no id-0 padding entries."""
+    base, q, g, codes, mn, mx, view = _sq8_setup(native, orc, 1200, 64, 8, metric, 11 + metric, 2)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, metric)
+    dev.set_graph(g)
+    dev.set_sq8(codes, mn, mx, 2)
+    k, ef = 10, 48
+    ids, d, _ = dev.search_sq8(q, k, ef, 2)
+    for i in range(len(q)):
+        pool_ids, _ = view.search(q[i], ef, ef)  # the search's whole pool, in pool order
+        ex = np.array([orc.dist(metric, q[i], base[j]) for j in pool_ids], np.float32)
+        order = sorted(range(ef), key=lambda j: (ex[j], pool_ids[j]))[:k]
+        assert np.array_equal(ids[i], pool_ids[order]), (i, ids[i], pool_ids[order])
+        assert np.array_equal(d[i].view(np.uint32), ex[order].view(np.uint32))
+        assert len(set(ids[i].tolist())) == k
+    # a pool shorter than ef (tiny graph): slots past the candidates are (0, 0.0)
+    small = base[:20].copy()
+    gs = native.Graph.build(small, metric, 32, 100, 1, 100)
+    mn2, mx2 = native.sq8_train(small)
+    dev2 = native.DeviceIndex(0)
+    dev2.set_base(small, metric)
+    dev2.set_graph(gs)
+    dev2.set_sq8(native.sq8_encode(small, mn2, mx2, 1), mn2, mx2, 2)
+    ids2, d2, _ = dev2.search_sq8(q[:1], 25, 40, 2)
+    assert sorted(ids2[0][:20].tolist()) == list(range(20))
+    assert ids2[0][20:].tolist() == [0] * 5 and d2[0][20:].tolist() == [0.0] * 5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
 def test_sq8_index_api(native, orc, metric, tmp_path):
     import alayalite_amd

@@ -52,6 +52,7 @@ def main():
     for i, nme in enumerate(names):
         per = mean[i] / exp if i not in (5, 6) else mean[i]
         print(f"  {nme:20s} mean/query {mean[i]:14.1f}   per expansion {mean[i]/exp:10.1f}")
+    print(f"  adjacency prefetch hits {mean[7]:.1f} per query = {mean[7] / exp:.3f} of expansions")
     print(f"  max query_total {st[:,6].max()}  min {st[:,6].min()}  p50 {np.median(st[:,6])}")
     if args.out:
         np.save(args.out, st)
