@@ -108,7 +108,7 @@ struct alaya_index {
   bool has_sq8 = false;
   int sq8_order = 2;
   uint32_t code_stride = 0;
-  DevBuf codes, sq_min, sq_max, rr_q_buf;
+  DevBuf codes, sq_min, sq_max, rr_q_buf, sq_ids, sq_d;
   // flat path
   DevBuf norms, cand_d, cand_i, flag_buf, iota;
   bool norms_ready = false;
@@ -637,51 +637,69 @@ int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint3
   });
 }
 
+// SQ8 graph search (+ optional rerank) on device buffers.  The search writes its ks = k (reference
+// rerank) or ef (corrected rerank) ids into ix->sq_ids; the rerank reads them and writes d_ids.
+static void sq8_search_dev(alaya_index *ix, const float *d_q, const float *d_rq, uint64_t nq, uint32_t k,
+                           uint32_t ef, int rerank, uint32_t *d_ids, float *d_dists, uint32_t *d_cnt,
+                           hipStream_t s) {
+  if (rerank < 0 || rerank > 2) throw ArgError("rerank must be 0 (none), 1 (reference) or 2 (corrected)");
+  if (nq == 0 || k == 0) return;
+  if (!rerank) {
+    do_search(ix, d_q, nq, k, ef, d_ids, d_dists, d_cnt, s, nullptr, true);
+    return;
+  }
+  const uint32_t ks = rerank == 2 ? ef : k;  // corrected: the whole ef pool, kEmpty past the pool
+  ix->sq_ids.reserve(nq * ks * 4);
+  ix->sq_d.reserve(nq * ks * 4);
+  do_search(ix, d_q, nq, ks, ef, ix->sq_ids.as<uint32_t>(), ix->sq_d.as<float>(), d_cnt, s, nullptr, true,
+            rerank == 2 ? 0xffffffffu : 0u);
+  SearchParams p = base_params(ix);
+  p.queries = d_rq ? d_rq : d_q;
+  p.nq = nq;
+  p.q_stride = ix->dim;
+  alaya_amd::RerankParams r{ix->sq_ids.as<uint32_t>(), k, ef, ks, rerank == 2 ? 1 : 0, d_ids, d_dists};
+  hip_check(alaya_amd::launch_rerank(p, r, s), "rerank launch");
+}
+
 int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
                                  uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
                                  float *dists, uint32_t *counters) {
   return guarded([&] {
     if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
-    if (rerank < 0 || rerank > 2) throw ArgError("rerank must be 0 (none), 1 (reference) or 2 (corrected)");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
     if (nq == 0 || k == 0) return;
-    // corrected rerank: the search hands over its whole ef pool (kEmpty past the pool)
-    const uint32_t ks = rerank == 2 ? ef : k;
     ix->q_buf.reserve(nq * ix->dim * 4);
-    ix->id_buf.reserve(nq * ks * 4);
-    ix->dist_buf.reserve(nq * ks * 4);
+    ix->id_buf.reserve(nq * k * 4);
+    ix->dist_buf.reserve(nq * k * 4);
     ix->cnt_buf.reserve(nq * 16);
     hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
-    do_search(ix, ix->q_buf.as<float>(), nq, ks, ef, ix->id_buf.as<uint32_t>(), ix->dist_buf.as<float>(),
-              ix->cnt_buf.as<uint32_t>(), ix->stream, nullptr, true, rerank == 2 ? 0xffffffffu : 0u);
-    uint32_t *final_ids = ix->id_buf.as<uint32_t>();
-    float *final_d = ix->dist_buf.as<float>();
-    if (rerank) {
-      ix->dlist_buf.reserve(nq * k * 4);
-      ix->dout_buf.reserve(nq * k * 4);
-      const float *rq = ix->q_buf.as<float>();
-      if (rerank_queries && rerank_queries != queries) {
-        ix->rr_q_buf.reserve(nq * ix->dim * 4);
-        hip_check(hipMemcpyAsync(ix->rr_q_buf.ptr, rerank_queries, nq * ix->dim * 4, hipMemcpyHostToDevice,
-                                 ix->stream), "H2D");
-        rq = ix->rr_q_buf.as<float>();
-      }
-      SearchParams p = base_params(ix);
-      p.queries = rq;
-      p.nq = nq;
-      p.q_stride = ix->dim;
-      alaya_amd::RerankParams r{ix->id_buf.as<uint32_t>(), k, ef, ks, rerank == 2 ? 1 : 0,
-                                ix->dlist_buf.as<uint32_t>(), ix->dout_buf.as<float>()};
-      hip_check(alaya_amd::launch_rerank(p, r, ix->stream), "rerank launch");
-      final_ids = ix->dlist_buf.as<uint32_t>();
-      final_d = ix->dout_buf.as<float>();
+    const float *d_rq = nullptr;
+    if (rerank && rerank_queries && rerank_queries != queries) {
+      ix->rr_q_buf.reserve(nq * ix->dim * 4);
+      hip_check(hipMemcpyAsync(ix->rr_q_buf.ptr, rerank_queries, nq * ix->dim * 4, hipMemcpyHostToDevice,
+                               ix->stream), "H2D");
+      d_rq = ix->rr_q_buf.as<float>();
     }
-    hip_check(hipMemcpyAsync(ids, final_ids, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
-    if (dists) hip_check(hipMemcpyAsync(dists, final_d, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    sq8_search_dev(ix, ix->q_buf.as<float>(), d_rq, nq, k, ef, rerank, ix->id_buf.as<uint32_t>(),
+                   ix->dist_buf.as<float>(), ix->cnt_buf.as<uint32_t>(), ix->stream);
+    hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    if (dists) hip_check(hipMemcpyAsync(dists, ix->dist_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     if (counters)
       hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");
     hip_check(hipStreamSynchronize(ix->stream), "sq8 search");
+  });
+}
+
+int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
+                                        uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *d_ids,
+                                        float *d_dists, uint32_t *d_counters, void *stream) {
+  return guarded([&] {
+    if (!ix || (nq && (!d_queries || !d_ids))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    sq8_search_dev(ix, d_queries, d_rerank_queries, nq, k, ef, rerank, d_ids, d_dists, d_counters,
+                   static_cast<hipStream_t>(stream));
   });
 }
 

@@ -38,6 +38,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 K = 10
 R = 32
 
+# HNSW workloads (BASELINE.json configs; generators and seeds in workloads/datasets.py)
+WORKLOADS = {
+    "gist-hnsw": {"gen": "gist_like", "dim": 960, "nq": 1000, "metric": 0, "sq8": False,
+                  "metric_name": "QPS @ recall@10>=0.95, GIST-960 L2, 1M base / 1k queries",
+                  "data": "synthetic (GIST-shaped 1024-centre low-rank mixture, seeds 5/6; graph built by the "
+                          "engine's HNSW builder R=32 efc=100)"},
+    "sift-hnsw": {"gen": "sift_like", "dim": 128, "nq": 10000, "metric": 0, "sq8": False,
+                  "metric_name": "QPS @ recall@10>=0.95, SIFT-128 L2, 1M base / 10k queries (config 3)",
+                  "data": "synthetic (SIFT-shaped 1024-centre mixture, integer-valued, seeds 3/4; graph built by "
+                          "the engine's HNSW builder R=32 efc=100)"},
+    "sq8-ip": {"gen": "text_like", "dim": 768, "nq": 1000, "metric": 1, "sq8": True,
+               "metric_name": "QPS @ recall@10>=0.95, 768-d IP, SQ8 search + f32 rerank, 1M base / 1k queries "
+                              "(config 5 shape at 1M)",
+               "data": "synthetic (text-embedding-shaped 4096-centre unit-sphere mixture, row-normalised, seeds 7/8; "
+                       "graph built on f32 rows with IP, R=32 efc=100; SQ8 codes of the same rows)"},
+}
+
 
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
@@ -50,8 +67,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--n", type=int, default=1_000_000)
-    p.add_argument("--nq", type=int, default=1000)
-    p.add_argument("--dim", type=int, default=960)
+    p.add_argument("--nq", type=int, default=0, help="0 = the workload's default")
+    p.add_argument("--dim", type=int, default=0, help="0 = the workload's default")
     p.add_argument("--efc", type=int, default=100)
     p.add_argument("--ef", type=int, default=0, help="fixed ef (skip the recall sweep)")
     p.add_argument("--target-recall", type=float, default=0.95)
@@ -61,9 +78,20 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cache-dir", default=os.path.join(ROOT, "data_cache"))
     p.add_argument("--dump-counters", default="")
-    p.add_argument("--workload", choices=("gist-hnsw", "flat"), default="gist-hnsw",
-                   help="gist-hnsw: the BASELINE metric (default); flat: config 2, 1M x 128 exact k-NN")
-    return p.parse_args()
+    p.add_argument("--workload", choices=tuple(WORKLOADS) + ("flat",), default="gist-hnsw",
+                   help="gist-hnsw: the BASELINE metric (default); sift-hnsw: config 3; sq8-ip: config 5 "
+                        "shape (768-d IP, SQ8 search + rerank); flat: config 2, 1M x 128 exact k-NN")
+    p.add_argument("--sweep-qps", action="store_true",
+                   help="also time every ef of the sweep (config 3 reports the whole QPS/recall curve)")
+    a = p.parse_args()
+    if a.workload in WORKLOADS:
+        w = WORKLOADS[a.workload]
+        a.nq = a.nq or w["nq"]
+        a.dim = a.dim or w["dim"]
+    else:
+        a.nq = a.nq or 1000
+        a.dim = a.dim or 128
+    return a
 
 
 def host_threads():
@@ -73,7 +101,7 @@ def host_threads():
         return max(1, min(16, os.cpu_count() or 1))
 
 
-def graph_for(native, base, efc, threads, cache_dir, tag):
+def graph_for(native, base, efc, threads, cache_dir, tag, metric=0):
     """Build (or load a cached copy of) the HNSW graph of `base` with the engine's host builder."""
     key = hashlib.md5(base[:: max(1, base.shape[0] // 4096)].tobytes()).hexdigest()[:12]
     path = os.path.join(cache_dir, f"{tag}_n{base.shape[0]}_d{base.shape[1]}_efc{efc}_{key}.index")
@@ -86,7 +114,7 @@ def graph_for(native, base, efc, threads, cache_dir, tag):
         except Exception as exc:  # corrupt cache: rebuild
             log("cache unusable:", exc)
     t = time.time()
-    g = native.Graph.build(base, 0, R, efc, threads, 100)
+    g = native.Graph.build(base, metric, R, efc, threads, 100)
     dt = time.time() - t
     log(f"built graph {base.shape} in {dt:.1f}s with {threads} threads")
     try:
@@ -98,17 +126,20 @@ def graph_for(native, base, efc, threads, cache_dir, tag):
     return g, dt
 
 
-def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64):
-    """Exact L2 top-k: fp32 GEMM shortlist on the device, float64 re-rank on the host."""
-    bn = (base_dev * base_dev).sum(1)
+def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64, metric=0):
+    """Exact top-k (L2, or IP = largest inner product): fp32 GEMM shortlist on the device, float64
+    re-rank on the host."""
+    bn = (base_dev * base_dev).sum(1) if metric == 0 else None
     out = np.zeros((queries_host.shape[0], k), np.int64)
     for s in range(0, queries_dev.shape[0], 256):
         q = queries_dev[s:s + 256]
-        d = bn[None, :] - 2.0 * (q @ base_dev.T)
+        d = bn[None, :] - 2.0 * (q @ base_dev.T) if metric == 0 else -(q @ base_dev.T)
         idx = torch.topk(d, cand, dim=1, largest=False).indices.cpu().numpy()
         for j in range(idx.shape[0]):
             c = idx[j]
-            dd = ((base_host[c].astype(np.float64) - queries_host[s + j].astype(np.float64)) ** 2).sum(1)
+            x = base_host[c].astype(np.float64)
+            y = queries_host[s + j].astype(np.float64)
+            dd = ((x - y) ** 2).sum(1) if metric == 0 else -(x @ y)
             out[s + j] = c[np.lexsort((c, dd))][:k]
     return out
 
@@ -227,6 +258,8 @@ def main():
     import torch
     import torch.distributed as dist
 
+    w = WORKLOADS[args.workload]
+    metric, use_sq8 = w["metric"], w["sq8"]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -237,28 +270,37 @@ def main():
 
     from alayalite_amd import _native
     from alayalite_amd.sharded import exchange_and_merge, shard_range
-    from workloads.datasets import gist_like
+    import workloads.datasets as datasets
 
     native = _native._ext
     threads = args.build_threads or host_threads()
 
     t0 = time.time()
-    base, queries = gist_like(args.n, args.nq, args.dim)
+    base, queries = getattr(datasets, w["gen"])(args.n, args.nq, args.dim)
     log(f"data {base.shape} + {queries.shape} in {time.time() - t0:.1f}s")
 
     # ---- index (shard or replica) ------------------------------------------------------------
     if world > 1 and args.mode == "shard":
         lo, hi = shard_range(args.n, world, rank)
         my_base = np.ascontiguousarray(base[lo:hi])
-        tag = f"gist_shard{rank}of{world}"
+        tag = f"{w['gen']}_m{metric}_shard{rank}of{world}"
     else:
         lo, hi = 0, args.n
         my_base = base
-        tag = "gist"
-    graph, build_s = graph_for(native, my_base, args.efc, threads, args.cache_dir, tag)
+        tag = f"{w['gen']}_m{metric}" if w["gen"] != "gist_like" else "gist"
+    graph, build_s = graph_for(native, my_base, args.efc, threads, args.cache_dir, tag, metric)
     index = native.DeviceIndex(local)
-    index.set_base(my_base, 0)
+    index.set_base(my_base, metric)
     index.set_graph(graph)
+    sq8 = None
+    if use_sq8:
+        # SQ8Space::fit on the shard's rows (sq8_space.hpp:116-127); reduction order of the host's
+        # get_*_sq8_func choice (AVX-512 -> 2, else AVX2 -> 1), as the reference would run here.
+        mn, mx = native.sq8_train(my_base)
+        codes = native.sq8_encode(my_base, mn, mx, threads)
+        order = native.host_sq8_order()
+        index.set_sq8(codes, mn, mx, order)
+        sq8 = (codes, mn, mx, order)
 
     q_dev = torch.from_numpy(queries).to(dev)
     nq = q_dev.shape[0]
@@ -267,9 +309,16 @@ def main():
     cnt_dev = torch.empty((nq, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    def launch(ef):
+        if use_sq8:  # SQ8 graph search + PyIndex::rerank as batch_search runs it (rerank mode 1)
+            index.search_sq8_device(q_dev.data_ptr(), 0, nq, K, ef, 1, ids_dev.data_ptr(), dists_dev.data_ptr(),
+                                    cnt_dev.data_ptr(), stream.cuda_stream)
+        else:
+            index.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
+                                cnt_dev.data_ptr(), stream.cuda_stream)
+
     def step(ef):
-        index.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
-                            cnt_dev.data_ptr(), stream.cuda_stream)
+        launch(ef)
         if world > 1 and args.mode == "shard":
             return exchange_and_merge(ids_dev, dists_dev, lo, K)
         return ids_dev, dists_dev
@@ -277,9 +326,10 @@ def main():
     # ---- ground truth + operating point ------------------------------------------------------
     if rank == 0:
         base_dev = torch.from_numpy(base).to(dev)
-        gt = exact_gt(torch, base_dev, q_dev, base, queries)
+        gt = exact_gt(torch, base_dev, q_dev, base, queries, metric=metric)
         del base_dev
         torch.cuda.empty_cache()
+
     def probe(ef):
         """recall@10 >= target at this ef (decided on rank 0, broadcast to every rank)."""
         ids, _ = step(ef)
@@ -303,42 +353,56 @@ def main():
     else:
         ef = choose_ef(probe)
 
+    def timed(ef_t, steps, warmup):
+        for _ in range(warmup):
+            step(ef_t)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record(stream)
+            launch(ef_t)
+            ev[i][1].record(stream)
+            if world > 1 and args.mode == "shard":
+                # exchange + merge of the same step (the search above is the per-shard kernel)
+                exchange_and_merge(ids_dev, dists_dev, lo, K)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t_start
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el, float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # ---- the QPS/recall curve (config 3 reports the sweep) ------------------------------------
+    curve = None
+    if args.sweep_qps and world == 1:
+        curve = []
+        for pt in sorted(sweep, key=lambda x: x["ef"]):
+            el, kms = timed(pt["ef"], max(3, args.steps // 4), 1)
+            curve.append({"ef": pt["ef"], "recall": pt["recall"], "qps": round(nq * max(3, args.steps // 4) / el, 1),
+                          "kernel_ms": round(kms, 4)})
+            log("curve", curve[-1])
+
     # ---- timed region ------------------------------------------------------------------------
-    for _ in range(args.warmup):
-        step(ef)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        index.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
-                            cnt_dev.data_ptr(), stream.cuda_stream)
-        ev[i][1].record(stream)
-        if world > 1 and args.mode == "shard":
-            # exchange + merge of the same step (the search above is the per-shard kernel)
-            exchange_and_merge(ids_dev, dists_dev, lo, K)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    elapsed, kernel_ms = timed(ef, args.steps, args.warmup)
 
     # ---- algorithmic bytes from the kernel's counters -------------------------
     cnt = cnt_dev.cpu().numpy().astype(np.int64)
-    row_bytes = 4 * args.dim
+    row_bytes = args.dim if use_sq8 else 4 * args.dim  # SQ8 codes are 1 B per dimension
     per_q = (row_bytes * (cnt[:, 0] + cnt[:, 2]) + 4 * R * cnt[:, 1] + 4 * R * cnt[:, 3]
              + 4 * args.dim + 8 * K)
+    if use_sq8:  # the rerank reads ef ids' f32 rows (k real + ef-k zero entries -> row 0 once)
+        per_q = per_q + 4 * args.dim * (K + (1 if ef > K else 0))
     bytes_launch = float(per_q.sum())
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
     prof = pmc_traffic({"n_base": args.n, "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef})
-    if prof is not None:
+    if prof is not None and not use_sq8 and args.workload == "gist-hnsw":
         # measured HBM bytes per algorithmic byte (PMC, gfx950-corrected) x this launch's bytes
         traffic_bytes = prof[1]["traffic_over_algorithmic"] * bytes_launch
         traffic = {"gbs": round(traffic_bytes / (kernel_ms * 1e-3) / 1e9, 1),
@@ -353,30 +417,13 @@ def main():
     # ---- CPU baseline: the reference's coroutine batch_search restated (oracle/) --------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle
-
-        oracle.build()
-        l0, levels, off, ue, ep, upper_r, _ = graph.arrays()
-        view = oracle.IndexView(base, l0, levels, off, ue, upper_r, ep)
-        ct = args.cpu_threads or host_threads()
-        runs = []
-        cpu_ids = None
-        budget = time.time() + 30.0
-        view.batch_search(queries, K, ef, ct)  # warm-up
-        while len(runs) < 5 and (time.time() < budget or not runs):
-            cpu_ids, _, _, sec = view.batch_search(queries, K, ef, ct)
-            runs.append(sec)
-        med = float(np.median(runs))
-        parity = bool(np.array_equal(cpu_ids, ids_dev.cpu().numpy().astype(np.uint32)))
-        cpu = {"value": round(nq / med, 1), "unit": "queries/s", "cores": ct, "kind": "port",
-               "sample": f"all {nq} queries at ef={ef}, median of {len(runs)} runs after 1 warm-up "
-                         f"(Scheduler begin->join), ids_equal_to_device={parity}"}
+        cpu = cpu_baseline(args, graph, base, queries, ef, metric, sq8, ids_dev.cpu().numpy().astype(np.uint32))
         log("cpu baseline", cpu)
 
     if rank == 0:
         r_at = next((s["recall"] for s in sweep if s["ef"] == ef), None)
         out = {
-            "metric": "QPS @ recall@10>=0.95, GIST-960 L2, 1M base / 1k queries",
+            "metric": w["metric_name"],
             "value": round(value, 1),
             "unit": "queries/s",
             "n_gpus": world,
@@ -386,11 +433,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if (world > 1 and args.mode == "replica") else "strong",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (GIST-shaped 1024-centre low-rank mixture, seeds 5/6; graph built by the engine's HNSW builder R=32 efc=100)",
-            "config": {"workload": f"hnsw-gist{args.dim}-{args.n // 1000}k-l2-{nq}q", "n_base": args.n,
-                       "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef, "recall_at_10": r_at,
-                       "ef_sweep": sweep, "mode": args.mode if world > 1 else "single",
+            "dtype": "u8+f32" if use_sq8 else "f32",
+            "data": w["data"],
+            "config": {"workload": f"hnsw-{w['gen'].split('_')[0]}{args.dim}-{args.n // 1000}k-"
+                                   f"{'ip-sq8' if use_sq8 else ('ip' if metric else 'l2')}-{nq}q",
+                       "n_base": args.n, "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef,
+                       "recall_at_10": r_at, "ef_sweep": sweep, "mode": args.mode if world > 1 else "single",
                        "parallelism": f"{args.mode}{world}" if world > 1 else "1gpu",
                        "graph_build_s": round(build_s, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -398,15 +446,59 @@ def main():
                          "traffic": traffic["gbs"] if traffic else None,
                          "traffic_bytes_per_launch": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": "hnsw_search_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": "hnsw_search_kernel" + ("+rerank_kernel" if use_sq8 else ""),
+                         "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": int(bytes_launch),
                          "mean_n_dist": round(float(cnt[:, 0].mean()), 1),
                          "mean_n_expand": round(float(cnt[:, 1].mean()), 1)},
             "cpu_baseline": cpu,
         }
+        if curve is not None:
+            out["config"]["qps_curve"] = curve
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline(args, graph, base, queries, ef, metric, sq8, device_ids):
+    """The oracle's coroutine batch driver (Scheduler/Worker restatement, AVX2 kernels) at the same
+    ef on this host's cores; SQ8 adds the post-join single-thread rerank loop (index.hpp:337-345).
+    Bounded sample: the whole batch when it fits ~30 s of CPU, else a prefix of the queries."""
+    import oracle
+
+    oracle.build()
+    l0, levels, off, ue, ep, upper_r, _ = graph.arrays()
+    view = oracle.IndexView(base, l0, levels, off, ue, upper_r, ep, metric=metric,
+                            sq8=None if sq8 is None else (sq8[0], sq8[1], sq8[2], sq8[3]))
+    ct = args.cpu_threads or host_threads()
+    nq = queries.shape[0]
+
+    def run(qs):
+        ids, _, _, sec = view.batch_search(qs, K, ef, ct)
+        if sq8 is not None:
+            ids, _, rsec = view.batch_rerank(qs, ids, K, ef)
+            sec += rsec
+        return ids, sec
+
+    # size the sample: time a small prefix first
+    probe_n = min(nq, 100)
+    _, t_probe = run(queries[:probe_n])
+    per_q = t_probe / probe_n
+    m = nq if per_q * nq <= 30.0 else max(probe_n, int(30.0 / max(per_q, 1e-9)))
+    sample = queries[:m]
+    runs, cpu_ids = [], None
+    budget = time.time() + 45.0
+    run(sample)  # warm-up
+    while len(runs) < 5 and (time.time() < budget or not runs):
+        cpu_ids, sec = run(sample)
+        runs.append(sec)
+    med = float(np.median(runs))
+    parity = bool(np.array_equal(cpu_ids, device_ids[:m]))
+    what = "search + rerank" if sq8 is not None else "search"
+    return {"value": round(m / med, 1), "unit": "queries/s", "cores": ct, "kind": "port",
+            "sample": f"{m} of {nq} queries at ef={ef} ({what}), median of {len(runs)} runs after 1 warm-up "
+                      f"(Scheduler begin->join{' + rerank loop' if sq8 is not None else ''}), "
+                      f"ids_equal_to_device={parity}"}
 
 
 if __name__ == "__main__":

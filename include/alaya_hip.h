@@ -114,6 +114,10 @@ int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint3
 int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
                                  uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
                                  float *dists, uint32_t *counters);
+/* Same on device buffers, asynchronous on `stream`; d_rerank_queries NULL = d_queries. */
+int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
+                                        uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *d_ids,
+                                        float *d_dists, uint32_t *d_counters, void *stream);
 /* ---- flat (exhaustive) exact k-NN, L2, dim <= 224, k <= 24 --------------------------------------
  * No reference implementation (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); the
  * analogue is find_exact_gt (include/utils/evaluate.hpp:29-62).  An f32-MFMA pass ranks every row

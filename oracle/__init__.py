@@ -100,6 +100,8 @@ def lib():
         _lib.orc_batch_search_coro.argtypes = [
             C.POINTER(OrcIndex), p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, p, p, p]
         _lib.orc_rerank.argtypes = [C.POINTER(OrcIndex), p, p, C.c_uint32, C.c_uint32, p, p]
+        _lib.orc_batch_rerank.restype = C.c_double
+        _lib.orc_batch_rerank.argtypes = [C.POINTER(OrcIndex), p, C.c_uint64, p, C.c_uint32, C.c_uint32, p, p]
         _lib.orc_sq8_fit.argtypes = [p, C.c_uint64, C.c_uint32, p, p]
         _lib.orc_sq8_encode.argtypes = [p, C.c_uint32, p, p, p]
         for name in ("orc_sq8_l2", "orc_sq8_ip"):
@@ -209,6 +211,16 @@ class IndexView:
         d = np.zeros(k, np.float32)
         lib().orc_rerank(C.byref(self.s), _ptr(q), _ptr(src), k, ef, _ptr(ids), _ptr(d))
         return ids, d
+
+    def batch_rerank(self, queries, search_ids, k, ef):
+        """The batch path's rerank loop (index.hpp:337-345); returns (ids, dists, seconds)."""
+        q = np.ascontiguousarray(queries, np.float32)
+        src = np.ascontiguousarray(search_ids, np.uint32)
+        nq = q.shape[0]
+        ids = np.zeros((nq, k), np.uint32)
+        d = np.zeros((nq, k), np.float32)
+        sec = lib().orc_batch_rerank(C.byref(self.s), _ptr(q), nq, _ptr(src), k, ef, _ptr(ids), _ptr(d))
+        return ids, d, sec
 
     def search(self, query, k, ef, with_counters=False):
         q = np.ascontiguousarray(query, np.float32)

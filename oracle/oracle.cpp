@@ -589,6 +589,16 @@ void orc_rerank(const orc_index *ix, const float *query, const uint32_t *search_
   }
 }
 
+// The Linux batch path's rerank loop after Scheduler::join (index.hpp:337-345): one thread, query
+// by query.  Returns its seconds (outside the reference's Timer, but part of batch_search).
+double orc_batch_rerank(const orc_index *ix, const float *queries, uint64_t nq, const uint32_t *search_ids,
+                        uint32_t k, uint32_t ef, uint32_t *ids, float *dists) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t i = 0; i < nq; ++i)
+    orc_rerank(ix, queries + i * ix->dim, search_ids + i * k, k, ef, ids + i * k, dists + i * k);
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 float orc_sq8_l2(const uint8_t *x, const uint8_t *y, size_t dim, const float *min_v,
                  const float *max_v, int variant) {
   return sq8_dist<false>(x, y, dim, min_v, max_v, variant);

@@ -107,6 +107,9 @@ double orc_batch_search_coro(const orc_index *ix, const float *queries, uint64_t
  * top-k by a min-heap on pair<dist, id>.  Writes k ids and their distances. */
 void orc_rerank(const orc_index *ix, const float *query, const uint32_t *search_ids, uint32_t k,
                 uint32_t ef, uint32_t *ids, float *dists);
+/* The batch path's rerank loop (index.hpp:337-345), single-threaded over nq queries; returns seconds. */
+double orc_batch_rerank(const orc_index *ix, const float *queries, uint64_t nq, const uint32_t *search_ids,
+                        uint32_t k, uint32_t ef, uint32_t *ids, float *dists);
 
 /* ---- SQ8 ---------------------------------------------------------------------------------- */
 void orc_sq8_fit(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v);

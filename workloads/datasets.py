@@ -5,6 +5,9 @@ component (32 shared latent directions) + small isotropic noise, clipped to [0, 
 a low intrinsic dimension; purely isotropic 960-d noise would make recall 0.95 unreachable at any
 practical ef, so the low-rank part is what puts recall 0.95 inside the ef sweep.
 SIFT-shaped (C3): 1024 centres ~ U[0, 128)^128, point = round(centre + N(0, 12^2)) clipped [0, 255].
+Text-embedding-shaped (C5): 4096 centres on the unit sphere, point = centre + low-rank component
+(48 latent directions) + small isotropic noise, row-normalised (inner product = cosine).  As for
+GIST, the low-rank part keeps recall 0.95 inside the ef sweep.
 """
 
 from __future__ import annotations
@@ -49,6 +52,29 @@ def sift_like(n: int, nq: int, dim: int = 128, seed_base: int = 3, seed_query: i
             k = r.integers(0, n_centres, e - s)
             x = np.rint(centres[k] + r.normal(0.0, 12.0, (e - s, dim)).astype(np.float32))
             np.clip(x, 0.0, 255.0, out=out[s:e])
+        return out
+
+    return draw(n, seed_base), draw(nq, seed_query)
+
+
+def text_like(n: int, nq: int, dim: int = 768, seed_base: int = 7, seed_query: int = 8,
+              n_centres: int = 4096, latent: int = 48, sigma_latent: float = 0.15,
+              sigma_noise: float = 0.01):
+    rng = np.random.default_rng(777)
+    centres = rng.standard_normal((n_centres, dim)).astype(np.float32)
+    centres /= np.linalg.norm(centres, axis=1, keepdims=True)
+    basis = (rng.standard_normal((latent, dim)) / np.sqrt(dim)).astype(np.float32)
+
+    def draw(count, seed):
+        r = np.random.default_rng(seed)
+        out = np.empty((count, dim), np.float32)
+        for s, e in _chunks(count):
+            k = r.integers(0, n_centres, e - s)
+            z = r.standard_normal((e - s, latent), dtype=np.float32) * sigma_latent
+            x = centres[k] + z @ basis
+            x += r.standard_normal((e - s, dim), dtype=np.float32) * sigma_noise
+            x /= np.linalg.norm(x, axis=1, keepdims=True)
+            out[s:e] = x
         return out
 
     return draw(n, seed_base), draw(nq, seed_query)
