@@ -14,6 +14,7 @@
 #include <thread>
 #include <vector>
 
+#include "graph_update.h"
 #include "hnsw_build.h"
 #include "flat_kernels.h"
 #include "search_kernels.h"
@@ -117,6 +118,11 @@ struct alaya_index {
   DevBuf work, overflow, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
   uint32_t hash_log2_override = 0;
   int num_cus = 0;
+  // online updates (alaya_index_enable_updates): host mirror + JobContext, device capacity
+  uint64_t capacity = 0;
+  std::unique_ptr<alaya_amd::HostGraph> upd_graph;
+  std::unique_ptr<alaya_amd::RowMirror> upd_rows;
+  std::unique_ptr<alaya_amd::UpdateContext> upd_ctx;
   hipStream_t stream = nullptr;
   uint64_t device_bytes() const {
     return base.bytes + valid.bytes + l0.bytes + levels.bytes + upper_off.bytes +
@@ -430,6 +436,10 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     ix->metric = metric;
     ix->overflow.release();
     ix->norms_ready = false;
+    ix->capacity = n;
+    ix->upd_graph.reset();
+    ix->upd_rows.reset();
+    ix->upd_ctx.reset();
   });
 }
 
@@ -472,6 +482,240 @@ int alaya_index_set_graph(alaya_index *ix, const alaya_graph *g) {
     ix->dedup = dup;
     ix->graph_n = h.n;
     ix->has_graph = true;
+    ix->upd_graph.reset();
+    ix->upd_rows.reset();
+    ix->upd_ctx.reset();
+  });
+}
+
+// ---- device mirror patches (online updates) ------------------------------------------------
+namespace {
+
+// Grow a device buffer to `bytes`, keeping its first `keep` bytes.
+void grow_keep(alaya_index *ix, DevBuf &b, size_t bytes, size_t keep) {
+  if (bytes <= b.bytes) return;
+  DevBuf nb;
+  nb.reserve(bytes);
+  hip_check(hipMemsetAsync(nb.ptr, 0, nb.bytes, ix->stream), "memset");
+  if (keep && b.ptr) hip_check(hipMemcpyAsync(nb.ptr, b.ptr, keep, hipMemcpyDeviceToDevice, ix->stream), "copy");
+  hip_check(hipStreamSynchronize(ix->stream), "sync");
+  std::swap(b.ptr, nb.ptr);
+  std::swap(b.bytes, nb.bytes);
+}
+
+void reserve_locked(alaya_index *ix, uint64_t capacity) {
+  if (!ix->base.ptr) throw ArgError("index has no base vectors");
+  if (capacity < ix->n) throw ArgError("capacity below the stored rows");
+  const size_t row = static_cast<size_t>(ix->stride) * 4;
+  grow_keep(ix, ix->base, std::max<uint64_t>(capacity, 1) * row, ix->n * row);
+  const size_t words = (std::max<uint64_t>(capacity, 1) + 31) / 32;
+  if (!ix->has_valid) {  // all stored rows valid: materialise the bitmap so rows can be removed
+    std::vector<uint32_t> w(words, 0u);
+    for (uint64_t i = 0; i < ix->n; ++i) w[i >> 5] |= 1u << (i & 31);
+    ix->valid.release();
+    ix->valid.reserve(words * 4);
+    hip_check(hipMemcpyAsync(ix->valid.ptr, w.data(), words * 4, hipMemcpyHostToDevice, ix->stream), "bitmap");
+    hip_check(hipStreamSynchronize(ix->stream), "sync");
+    ix->has_valid = true;
+  } else {
+    grow_keep(ix, ix->valid, words * 4, (ix->n + 31) / 32 * 4);
+  }
+  if (ix->has_graph) {
+    grow_keep(ix, ix->l0, std::max<uint64_t>(capacity, 1) * ix->R * 4, ix->graph_n * ix->R * 4);
+    grow_keep(ix, ix->levels, std::max<uint64_t>(capacity, 1) * 4, ix->graph_n * 4);
+    grow_keep(ix, ix->upper_off, std::max<uint64_t>(capacity, 1) * 8, ix->graph_n * 8);
+  }
+  ix->capacity = std::max(ix->capacity, capacity);
+}
+
+void write_rows_locked(alaya_index *ix, uint64_t first, const float *rows, uint64_t count) {
+  const size_t row = static_cast<size_t>(ix->stride) * 4;
+  if (first + count > ix->capacity || (first + count) * row > ix->base.bytes)
+    throw ArgError("rows beyond the reserved capacity");
+  char *dst = static_cast<char *>(ix->base.ptr) + first * row;
+  hip_check(hipMemset2DAsync(dst, row, 0, row, count, ix->stream), "memset");
+  hip_check(hipMemcpy2DAsync(dst, row, rows, static_cast<size_t>(ix->dim) * 4, static_cast<size_t>(ix->dim) * 4,
+                             count, hipMemcpyHostToDevice, ix->stream), "write rows");
+  hip_check(hipStreamSynchronize(ix->stream), "sync");
+  ix->n = std::max(ix->n, first + count);
+  ix->norms_ready = false;
+}
+
+void write_edges_locked(alaya_index *ix, const uint32_t *ids, const uint32_t *edges, uint64_t count) {
+  if (!ix->has_graph) throw ArgError("index has no graph");
+  for (uint64_t i = 0; i < count; ++i) {
+    if (ids[i] >= ix->capacity || ids[i] >= ix->n || (static_cast<uint64_t>(ids[i]) + 1) * ix->R * 4 > ix->l0.bytes ||
+        (ix->has_overlay && (static_cast<uint64_t>(ids[i]) + 1) * 4 > ix->levels.bytes))
+      throw ArgError("edge row id out of range (reserve capacity first)");
+    const uint32_t *r = edges + i * ix->R;
+    for (uint32_t a = 0; a < ix->R && r[a] != 0xffffffffu; ++a) {
+      for (uint32_t b = 0; b < a; ++b)
+        if (r[a] == r[b]) ix->dedup = true;  // e.g. the zero padding update() writes
+    }
+    hip_check(hipMemcpyAsync(ix->l0.as<uint32_t>() + static_cast<uint64_t>(ids[i]) * ix->R, r, ix->R * 4,
+                             hipMemcpyHostToDevice, ix->stream), "write edges");
+    ix->graph_n = std::max<uint64_t>(ix->graph_n, static_cast<uint64_t>(ids[i]) + 1);
+  }
+  hip_check(hipStreamSynchronize(ix->stream), "sync");
+}
+
+void set_valid_locked(alaya_index *ix, uint64_t id, bool valid) {
+  if (!ix->has_valid || id >= ix->capacity || (id / 32 + 1) * 4 > ix->valid.bytes)
+    throw ArgError("id out of range (reserve capacity first)");
+  uint32_t w = 0;
+  uint32_t *dw = ix->valid.as<uint32_t>() + (id >> 5);
+  hip_check(hipMemcpy(&w, dw, 4, hipMemcpyDeviceToHost), "read bitmap");
+  w = valid ? (w | (1u << (id & 31))) : (w & ~(1u << (id & 31)));
+  hip_check(hipMemcpy(dw, &w, 4, hipMemcpyHostToDevice), "write bitmap");
+}
+
+}  // namespace
+
+int alaya_index_reserve(alaya_index *ix, uint64_t capacity) {
+  return guarded([&] {
+    if (!ix) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    reserve_locked(ix, capacity);
+  });
+}
+
+int alaya_index_write_rows(alaya_index *ix, uint64_t first, const float *rows, uint64_t count) {
+  return guarded([&] {
+    if (!ix || (count && !rows)) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    write_rows_locked(ix, first, rows, count);
+  });
+}
+
+int alaya_index_write_edges(alaya_index *ix, const uint32_t *ids, const uint32_t *edges, uint64_t count) {
+  return guarded([&] {
+    if (!ix || (count && (!ids || !edges))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    write_edges_locked(ix, ids, edges, count);
+  });
+}
+
+int alaya_index_set_valid(alaya_index *ix, uint64_t id, int valid) {
+  return guarded([&] {
+    if (!ix) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    set_valid_locked(ix, id, valid != 0);
+  });
+}
+
+int alaya_index_enable_updates(alaya_index *ix, const alaya_graph *g, const float *rows, uint64_t n,
+                               uint64_t capacity, const uint8_t *valid_bitmap) {
+  return guarded([&] {
+    if (!ix || !g || (n && !rows)) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (g->g.n != n || ix->n != n || ix->graph_n != n) throw ArgError("graph, rows and device index sizes differ");
+    if (capacity < n) throw ArgError("capacity below the stored rows");
+    auto m = std::make_unique<alaya_amd::RowMirror>();
+    m->dim = ix->dim;
+    m->metric = ix->metric;
+    m->rows.assign(rows, rows + n * ix->dim);
+    m->valid.assign((capacity + 7) / 8 + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+      const bool v = valid_bitmap ? ((valid_bitmap[i >> 3] >> (i & 7)) & 1) : true;
+      if (v) m->valid[i >> 3] |= static_cast<uint8_t>(1u << (i & 7));
+    }
+    ix->upd_graph = std::make_unique<alaya_amd::HostGraph>(g->g);
+    ix->upd_rows = std::move(m);
+    ix->upd_ctx = std::make_unique<alaya_amd::UpdateContext>();
+    reserve_locked(ix, capacity);
+  });
+}
+
+int alaya_index_insert(alaya_index *ix, const float *search_query, const float *row, uint32_t ef,
+                       uint64_t *new_id) {
+  return guarded([&] {
+    if (!ix || !search_query || !row || !new_id) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (!ix->upd_graph) throw ArgError("updates are not enabled on this index");
+    alaya_amd::HostGraph &g = *ix->upd_graph;
+    alaya_amd::RowMirror &m = *ix->upd_rows;
+    alaya_amd::UpdateContext &ctx = *ix->upd_ctx;
+    const uint32_t R = g.R;
+    // search_solo(query, max_nbrs, results, ef) on the current index (graph_update_job.hpp:67-69)
+    std::vector<uint32_t> results(R, 0u);
+    ix->q_buf.reserve(static_cast<size_t>(ix->dim) * 4);
+    ix->id_buf.reserve(static_cast<size_t>(R) * 4);
+    hip_check(hipMemcpyAsync(ix->q_buf.ptr, search_query, ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
+    do_search(ix, ix->q_buf.as<float>(), 1, R, std::max(ef, 1u), ix->id_buf.as<uint32_t>(), nullptr, nullptr,
+              ix->stream);
+    hip_check(hipMemcpyAsync(results.data(), ix->id_buf.ptr, R * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+    hip_check(hipStreamSynchronize(ix->stream), "insert search");
+    // graph_->insert: -1 when the storage is full (then nothing else happens, :70-73)
+    if (g.n >= ix->capacity) {
+      *new_id = UINT64_MAX;
+      return;
+    }
+    const uint32_t id = static_cast<uint32_t>(g.n);
+    g.l0.insert(g.l0.end(), results.begin(), results.end());
+    if (g.has_overlay) {  // Graph::insert adds a level-0 node; the overlay is not touched
+      g.levels.push_back(0);
+      g.upper_off.push_back(g.upper_edges.size());
+    }
+    g.n += 1;
+    // space_->insert (RawSpace::insert: row stored, validity bit set)
+    m.rows.insert(m.rows.end(), row, row + ix->dim);
+    m.valid[id >> 3] |= static_cast<uint8_t>(1u << (id & 7));
+    for (uint32_t i = 0; i < R; ++i)
+      if (results[i] != 0xffffffffu) ctx.inserted_edges[results[i]].push_back(id);
+    // update every node that gained an edge (:80-83), in the map's iteration order
+    std::vector<uint32_t> touched{id};
+    std::vector<uint32_t> edges(results);
+    for (const auto &kv : ctx.inserted_edges) {
+      std::vector<uint32_t> e = alaya_amd::update_edges(g, m, ctx, kv.first);
+      std::copy(e.begin(), e.end(), g.l0.begin() + static_cast<size_t>(kv.first) * R);
+      touched.push_back(kv.first);
+      edges.insert(edges.end(), e.begin(), e.end());
+    }
+    ctx.inserted_edges.clear();
+    // mirror into HBM: the row, its validity bit, the new and the updated adjacency rows
+    write_rows_locked(ix, id, row, 1);
+    set_valid_locked(ix, id, true);
+    write_edges_locked(ix, touched.data(), edges.data(), touched.size());
+    *new_id = id;
+  });
+}
+
+int alaya_index_remove(alaya_index *ix, uint64_t id) {
+  return guarded([&] {
+    if (!ix) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (!ix->upd_graph) throw ArgError("updates are not enabled on this index");
+    if (id >= ix->upd_graph->n) throw ArgError("id out of range");
+    alaya_amd::record_remove(*ix->upd_graph, *ix->upd_ctx, static_cast<uint32_t>(id));
+    ix->upd_rows->valid[id >> 3] &= static_cast<uint8_t>(~(1u << (id & 7)));
+    set_valid_locked(ix, id, false);
+  });
+}
+
+int alaya_index_export_graph(alaya_index *ix, alaya_graph **out) {
+  return guarded([&] {
+    if (!ix || !out) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (!ix->upd_graph) throw ArgError("updates are not enabled on this index");
+    *out = new alaya_graph{*ix->upd_graph};
+  });
+}
+
+int alaya_index_export_rows(alaya_index *ix, float *rows, uint8_t *valid_bitmap, uint64_t *n) {
+  return guarded([&] {
+    if (!ix || !n) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (!ix->upd_rows) throw ArgError("updates are not enabled on this index");
+    *n = ix->upd_graph->n;
+    if (rows) std::memcpy(rows, ix->upd_rows->rows.data(), ix->upd_rows->rows.size() * 4);
+    if (valid_bitmap) std::memcpy(valid_bitmap, ix->upd_rows->valid.data(), (*n + 7) / 8);
   });
 }
 

@@ -130,6 +130,8 @@ class PyIndexInterface {
     raw_.assign(static_cast<const char *>(arr.data()),
                 static_cast<const char *>(arr.data()) + n * dim_ * dtype_size(dtype_));
     n_ = n;
+    delete_cnt_ = 0;
+    valid_.clear();
     rows_f32_.resize(n * dim_);
     to_float(raw_.data(), dtype_, n * dim_, rows_f32_.data());
     if (graph_) alaya_graph_free(graph_);
@@ -169,16 +171,62 @@ class PyIndexInterface {
     return out;
   }
 
-  py::object insert(py::array, uint32_t) {
-    throw std::runtime_error("insert is not implemented on the MI355X engine yet (SURVEY.md §8f F4)");
+  // PyIndex::insert -> GraphUpdateJob::insert_and_update (index.hpp:229-232,
+  // graph_update_job.hpp:65-89): device search_solo for R neighbours, host update job, HBM patch.
+  py::object insert(py::array insert_data, uint32_t ef) {
+    if (!graph_) throw std::runtime_error("Index is not init yet");
+    if (params_.quantization_type_ != QuantizationType::NONE)
+      throw std::runtime_error("insert on quantized indexes is not supported by the MI355X engine");
+    check_dtype(insert_data);
+    if (insert_data.ndim() != 1 || static_cast<uint32_t>(insert_data.shape(0)) != dim_)
+      throw std::runtime_error("vector dimension mismatch");
+    py::array arr = py::array::ensure(insert_data, py::array::c_style);
+    ensure_updates();
+    // COS: search_solo's QueryComputer normalises the caller's vector in place (raw_space.hpp:
+    // 267-269), then RawSpace::insert normalises it again (:146-150).
+    std::vector<float> q(dim_), row(dim_);
+    if (params_.metric_ == MetricType::COS) normalize_in_place(arr, 1);
+    to_float(arr.data(), dtype_, dim_, q.data());
+    if (params_.metric_ == MetricType::COS) normalize_in_place(arr, 1);
+    to_float(arr.data(), dtype_, dim_, row.data());
+    uint64_t id = 0;
+    {
+      py::gil_scoped_release nogil;
+      check(alaya_index_insert(ix_, q.data(), row.data(), ef, &id));
+    }
+    if (id == UINT64_MAX) return py::int_(id_bytes_ == 4 ? uint64_t{0xffffffffu} : UINT64_MAX);
+    const size_t es = dtype_size(dtype_);
+    raw_.insert(raw_.end(), static_cast<const char *>(arr.data()), static_cast<const char *>(arr.data()) + dim_ * es);
+    rows_f32_.insert(rows_f32_.end(), row.begin(), row.end());
+    n_ += 1;
+    if (!valid_.empty()) {
+      valid_.resize((n_ + 7) / 8, 0);
+      valid_[id / 8] |= static_cast<uint8_t>(1u << (id % 8));
+    }
+    graph_dirty_ = true;
+    return py::int_(id);
   }
-  void remove(uint32_t) {
-    throw std::runtime_error("remove is not implemented on the MI355X engine yet (SURVEY.md §8f F4)");
+
+  // PyIndex::remove -> GraphUpdateJob::remove (index.hpp:234, graph_update_job.hpp:91-103)
+  void remove(uint32_t id) {
+    if (!graph_) throw std::runtime_error("Index is not init yet");
+    if (params_.quantization_type_ != QuantizationType::NONE)
+      throw std::runtime_error("remove on quantized indexes is not supported by the MI355X engine");
+    if (id >= n_) throw std::runtime_error("id out of range");
+    ensure_updates();
+    check(alaya_index_remove(ix_, id));
+    if (valid_.empty()) {
+      valid_.assign((n_ + 7) / 8, 0);
+      for (uint64_t i = 0; i < n_; ++i) valid_[i / 8] |= static_cast<uint8_t>(1u << (i % 8));
+    }
+    valid_[id / 8] &= static_cast<uint8_t>(~(1u << (id % 8)));
+    delete_cnt_ += 1;  // RawSpace::remove counts every call (raw_space.hpp:160-163)
   }
 
   // PyIndex::save (index.hpp:113-130): graph file + raw data file (+ quant file)
   void save(const std::string &index_path, const std::string &data_path, const std::string &quant_path) {
     if (!graph_) throw std::runtime_error("index is not fitted");
+    sync_graph();
     check(alaya_graph_save(graph_, index_path.c_str(), id_bytes_, std::max<uint64_t>(params_.capacity_, n_)));
     if (!data_path.empty()) save_raw(data_path);
     if (!quant_path.empty()) {
@@ -226,8 +274,9 @@ class PyIndexInterface {
     return out;
   }
   // graph arrays (n x R l0, levels, upper_off, upper_edges, ep, upper_R) for tests/tools
-  py::tuple graph_arrays() const {
+  py::tuple graph_arrays() {
     if (!graph_) throw std::runtime_error("index is not fitted");
+    sync_graph();
     uint64_t n, nue;
     uint32_t R, upper_R, ep, max_level, n_eps;
     int has_overlay;
@@ -326,7 +375,26 @@ class PyIndexInterface {
     return {ids, want_dist ? py::array(dists) : py::array()};
   }
 
+  // first insert/remove: hand the device index a host mirror of the graph, rows and bitmap
+  void ensure_updates() {
+    if (updates_enabled_) return;
+    const uint64_t cap = std::max<uint64_t>(params_.capacity_, n_);
+    check(alaya_index_enable_updates(ix_, graph_, rows_f32_.data(), n_, cap, valid_.empty() ? nullptr : valid_.data()));
+    updates_enabled_ = true;
+  }
+  // replace the (stale) fitted graph with the updated mirror
+  void sync_graph() {
+    if (!graph_dirty_) return;
+    alaya_graph *g = nullptr;
+    check(alaya_index_export_graph(ix_, &g));
+    alaya_graph_free(graph_);
+    graph_ = g;
+    graph_dirty_ = false;
+  }
+
   void upload() {
+    updates_enabled_ = false;
+    graph_dirty_ = false;
     if (!graph_) return;
     uint64_t gn = 0;
     check(alaya_graph_info(graph_, &gn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
@@ -368,7 +436,7 @@ class PyIndexInterface {
       }
     };
     put_id(n_);   // item_cnt_
-    put_id(0);    // delete_cnt_
+    put_id(delete_cnt_);  // delete_cnt_
     put_id(cap);  // capacity_
     const uint64_t item = data_size, aligned = (item + 63) / 64 * 64, align = 64;
     w.write(reinterpret_cast<const char *>(&item), 8);
@@ -408,7 +476,7 @@ class PyIndexInterface {
       return x;
     };
     const uint64_t item_cnt = get_id();
-    (void)get_id();
+    delete_cnt_ = get_id();
     (void)get_id();
     uint64_t hdr[5];
     r.read(reinterpret_cast<char *>(hdr), sizeof(hdr));
@@ -522,6 +590,9 @@ class PyIndexInterface {
   std::vector<char> raw_;          // original-dtype rows (get_data_by_id, save)
   std::vector<float> rows_f32_;    // float rows uploaded to HBM
   std::vector<uint8_t> valid_;     // empty = all valid
+  uint64_t delete_cnt_ = 0;        // RawSpace::delete_cnt_
+  bool updates_enabled_ = false;   // the device index holds an update mirror (alaya_index_enable_updates)
+  bool graph_dirty_ = false;       // graph_ predates inserts (sync_graph refreshes it)
   std::vector<uint32_t> last_counters_;
   int rerank_mode_ = 1;
   std::vector<float> raw_queries_;   // SQ8 + COS: the un-normalised queries the SQ8 search encodes

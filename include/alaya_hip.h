@@ -88,6 +88,32 @@ int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq,
 int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uint64_t nq,
                                     uint32_t k, uint32_t ef, uint32_t *d_ids, float *d_dists,
                                     uint32_t *d_counters, void *stream);
+/* ---- online updates (Index.insert / Index.remove) ------------------------------------------
+ * Device-mirror primitives, for a host that keeps its own graph and update job (the reference's
+ * GraphUpdateJob, include/executor/jobs/graph_update_job.hpp:49-137) and patches HBM after each
+ * change:  reserve capacity (rows, validity, adjacency; contents kept), write rows at [first,
+ * first+count), overwrite level-0 adjacency rows, set or clear a validity bit
+ * (SequentialStorage::insert/remove, sequential_storage.hpp:77-100). */
+int alaya_index_reserve(alaya_index *ix, uint64_t capacity);
+int alaya_index_write_rows(alaya_index *ix, uint64_t first, const float *rows, uint64_t count);
+int alaya_index_write_edges(alaya_index *ix, const uint32_t *ids, const uint32_t *edges, uint64_t count);
+int alaya_index_set_valid(alaya_index *ix, uint64_t id, int valid);
+/* Or let the engine run the update job: enable_updates copies the graph, rows and bitmap into a
+ * host mirror (capacity = the index capacity, IndexParams.capacity_).  insert = PyIndex::insert ->
+ * insert_and_update (graph_update_job.hpp:65-89): search_solo for R neighbours at ef on the device,
+ * append the node, update() every node that gained an edge, patch HBM.  search_query is the query
+ * as search_solo sees it and row the vector as RawSpace::insert stores it (they differ only for COS,
+ * which normalises at both steps).  new_id = UINT64_MAX when the index is full.  remove =
+ * GraphUpdateJob::remove (:91-103): record the node's edges, clear its validity bit.  export_*
+ * return the mirror (for save). */
+int alaya_index_enable_updates(alaya_index *ix, const alaya_graph *g, const float *rows, uint64_t n,
+                               uint64_t capacity, const uint8_t *valid_bitmap);
+int alaya_index_insert(alaya_index *ix, const float *search_query, const float *row, uint32_t ef,
+                       uint64_t *new_id);
+int alaya_index_remove(alaya_index *ix, uint64_t id);
+int alaya_index_export_graph(alaya_index *ix, alaya_graph **out);
+/* rows: n x dim (nullable), valid_bitmap: (n+7)/8 bytes (nullable); *n = stored rows. */
+int alaya_index_export_rows(alaya_index *ix, float *rows, uint8_t *valid_bitmap, uint64_t *n);
 /* out[q*n + i] = metric distance(queries[q], row ids[i]), bit-exact with the search kernel. */
 int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, const uint32_t *ids,
                           uint32_t n, float *out);

@@ -100,6 +100,14 @@ def lib():
         _lib.orc_batch_search_coro.argtypes = [
             C.POINTER(OrcIndex), p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, p, p, p]
         _lib.orc_rerank.argtypes = [C.POINTER(OrcIndex), p, p, C.c_uint32, C.c_uint32, p, p]
+        _lib.orc_updater_new.restype = p
+        _lib.orc_updater_new.argtypes = [C.POINTER(OrcIndex), C.c_uint64]
+        _lib.orc_updater_free.argtypes = [p]
+        _lib.orc_updater_view.restype = C.POINTER(OrcIndex)
+        _lib.orc_updater_view.argtypes = [p]
+        _lib.orc_updater_insert.restype = C.c_int64
+        _lib.orc_updater_insert.argtypes = [p, p, p, C.c_uint32]
+        _lib.orc_updater_remove.argtypes = [p, C.c_uint32]
         _lib.orc_batch_rerank.restype = C.c_double
         _lib.orc_batch_rerank.argtypes = [C.POINTER(OrcIndex), p, C.c_uint64, p, C.c_uint32, C.c_uint32, p, p]
         _lib.orc_sq8_fit.argtypes = [p, C.c_uint64, C.c_uint32, p, p]
@@ -242,6 +250,45 @@ class IndexView:
         sec = lib().orc_batch_search_coro(C.byref(self.s), _ptr(q), nq, k, ef, num_threads,
                                           _ptr(ids), _ptr(dists), _ptr(cnt))
         return ids, dists, cnt, sec
+
+
+class Updater:
+    """GraphUpdateJob restated on a copy of an IndexView (graph_update_job.hpp:49-137)."""
+
+    def __init__(self, view: IndexView, capacity: int):
+        self._keep = view
+        self._h = lib().orc_updater_new(C.byref(view.s), capacity)
+        self.dim = view.base.shape[1]
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_updater_free(self._h)
+            self._h = None
+
+    def insert(self, search_query, row, ef):
+        q = np.ascontiguousarray(search_query, np.float32)
+        r = np.ascontiguousarray(row, np.float32)
+        return int(lib().orc_updater_insert(self._h, _ptr(q), _ptr(r), ef))
+
+    def remove(self, node):
+        lib().orc_updater_remove(self._h, node)
+
+    def _view(self):
+        return lib().orc_updater_view(self._h).contents
+
+    def n(self):
+        return int(self._view().n)
+
+    def l0(self):
+        v = self._view()
+        return np.ctypeslib.as_array(C.cast(v.l0, C.POINTER(C.c_uint32)), shape=(v.n, v.R)).copy()
+
+    def search(self, query, k, ef):
+        q = np.ascontiguousarray(query, np.float32)
+        ids = np.zeros(k, np.uint32)
+        d = np.zeros(k, np.float32)
+        lib().orc_search(lib().orc_updater_view(self._h), _ptr(q), k, ef, _ptr(ids), _ptr(d), None)
+        return ids, d
 
 
 def sq8_fit(data):

@@ -10,6 +10,8 @@
 #include <atomic>
 #include <cfloat>
 #include <chrono>
+#include <unordered_map>
+#include <unordered_set>
 #include <cmath>
 #include <coroutine>
 #include <cstring>
@@ -606,6 +608,125 @@ float orc_sq8_l2(const uint8_t *x, const uint8_t *y, size_t dim, const float *mi
 float orc_sq8_ip(const uint8_t *x, const uint8_t *y, size_t dim, const float *min_v,
                  const float *max_v, int variant) {
   return sq8_dist<true>(x, y, dim, min_v, max_v, variant);
+}
+
+
+// ---- online updates: GraphUpdateJob (include/executor/jobs/graph_update_job.hpp:49-137) ------
+// JobContext (job_context.hpp:25-29) with the reference's container types, so iteration orders
+// (and the LinearPool tie order in update()) follow the same libstdc++ sequences.
+struct orc_updater {
+  orc_index view;
+  uint64_t capacity;
+  std::vector<float> base;
+  std::vector<uint32_t> l0;
+  std::vector<uint8_t> valid;
+  std::vector<uint32_t> levels;
+  std::vector<uint64_t> upper_off;
+  std::vector<uint32_t> upper_edges;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> inserted_edges;
+  std::unordered_set<uint32_t> removed_vertices;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> removed_node_nbrs;
+
+  void refresh() {
+    view.base = base.data();
+    view.stride = view.dim;
+    view.l0 = l0.data();
+    view.valid = valid.data();
+    view.levels = levels.empty() ? nullptr : levels.data();
+    view.upper_off = upper_off.empty() ? nullptr : upper_off.data();
+    view.upper_edges = upper_edges.empty() ? nullptr : upper_edges.data();
+  }
+  float dist_by_id(uint32_t q, uint32_t u) const {  // QueryComputer(space, id) (raw_space.hpp:276-281)
+    if (!((valid[u >> 3] >> (u & 7)) & 1)) return FLT_MAX;
+    const float *x = base.data() + static_cast<size_t>(q) * view.dim;
+    const float *y = base.data() + static_cast<size_t>(u) * view.dim;
+    return view.metric == ORC_L2 ? orc_l2_f32(x, y, view.dim) : orc_ip_f32(x, y, view.dim);
+  }
+  void update(uint32_t node) {  // :105-137
+    std::unordered_set<uint32_t> candidate_nbrs;
+    const uint32_t R = view.R;
+    for (uint32_t i = 0; i < R; ++i) {
+      uint32_t nbr = l0[static_cast<size_t>(node) * R + i];
+      if (nbr == 0xffffffffu) break;
+      if (removed_vertices.count(nbr)) {
+        for (auto &second_hop_nbr : removed_node_nbrs.at(nbr)) candidate_nbrs.insert(second_hop_nbr);
+      }
+      candidate_nbrs.insert(nbr);
+    }
+    if (inserted_edges.count(node)) {
+      for (auto inserted_nbr : inserted_edges.at(node)) candidate_nbrs.insert(inserted_nbr);
+    }
+    Pool pool(view.n, static_cast<int>(R));
+    for (auto &nbr : candidate_nbrs) pool.insert(nbr, dist_by_id(node, nbr));
+    std::vector<uint32_t> updated_edges(R);  // value-initialised: zeros past the pool
+    for (uint32_t i = 0; i < R && i < pool.size; i++) updated_edges[i] = pool.id(i);
+    std::memcpy(&l0[static_cast<size_t>(node) * R], updated_edges.data(), R * 4);
+  }
+};
+
+orc_updater *orc_updater_new(const orc_index *ix, uint64_t capacity) {
+  auto *u = new orc_updater();
+  u->view = *ix;
+  u->capacity = capacity;
+  const uint64_t n = ix->n;
+  u->base.resize(n * ix->dim);
+  for (uint64_t i = 0; i < n; ++i)
+    std::memcpy(&u->base[i * ix->dim], ix->base + i * ix->stride, ix->dim * sizeof(float));
+  u->l0.assign(ix->l0, ix->l0 + n * ix->R);
+  u->valid.assign((capacity + 7) / 8 + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    const bool v = ix->valid ? ((ix->valid[i >> 3] >> (i & 7)) & 1) : true;
+    if (v) u->valid[i >> 3] |= static_cast<uint8_t>(1u << (i & 7));
+  }
+  if (ix->levels) {
+    u->levels.assign(ix->levels, ix->levels + n);
+    u->upper_off.assign(ix->upper_off, ix->upper_off + n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i)
+      if (ix->levels[i] > 0) total = std::max<uint64_t>(total, ix->upper_off[i] + uint64_t(ix->levels[i]) * ix->upper_R);
+    u->upper_edges.assign(ix->upper_edges, ix->upper_edges + total);
+  }
+  u->refresh();
+  return u;
+}
+
+void orc_updater_free(orc_updater *u) { delete u; }
+const orc_index *orc_updater_view(orc_updater *u) { return &u->view; }
+
+int64_t orc_updater_insert(orc_updater *u, const float *search_query, const float *row, uint32_t ef) {
+  const uint32_t R = u->view.R;
+  std::vector<uint32_t> search_results(R, 0xffffffffu);
+  orc_search(&u->view, search_query, R, ef, search_results.data(), nullptr, nullptr);
+  if (u->view.n >= u->capacity) return -1;  // Graph::insert fails: nothing else happens
+  const uint32_t node_id = static_cast<uint32_t>(u->view.n);
+  u->l0.insert(u->l0.end(), search_results.begin(), search_results.end());
+  if (!u->levels.empty()) {
+    u->levels.push_back(0);
+    u->upper_off.push_back(u->upper_edges.size());
+  }
+  u->base.insert(u->base.end(), row, row + u->view.dim);  // RawSpace::insert
+  u->valid[node_id >> 3] |= static_cast<uint8_t>(1u << (node_id & 7));
+  u->view.n += 1;
+  u->refresh();
+  for (uint32_t i = 0; i < R; i++) {
+    auto invert_node = search_results[i];
+    if (invert_node != 0xffffffffu) u->inserted_edges[invert_node].push_back(node_id);
+  }
+  for (const auto &kv : u->inserted_edges) u->update(kv.first);
+  u->inserted_edges.clear();
+  return node_id;
+}
+
+void orc_updater_remove(orc_updater *u, uint32_t node_id) {  // :91-103
+  const uint32_t R = u->view.R;
+  auto &rec = u->removed_node_nbrs[node_id];
+  for (uint32_t i = 0; i < R; i++) {
+    auto nbr = u->l0[static_cast<size_t>(node_id) * R + i];
+    if (nbr == 0xffffffffu) break;
+    rec.push_back(nbr);
+  }
+  u->removed_vertices.insert(node_id);
+  u->valid[node_id >> 3] &= static_cast<uint8_t>(~(1u << (node_id & 7)));
 }
 
 }  // extern "C"

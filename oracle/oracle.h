@@ -19,6 +19,9 @@
  *                                   GraphSearchJob::search (coroutine) graph_search_job.hpp:221-299
  *                                   on the Scheduler/Worker runtime (executor/scheduler.hpp:113-203,
  *                                   executor/worker.hpp:111-136, 4 local tasks per worker)
+ *   orc_updater_*                   GraphUpdateJob insert_and_update / update / remove
+ *                                   (executor/jobs/graph_update_job.hpp:49-137) with JobContext
+ *                                   (job_context.hpp:25-29), Graph/RawSpace insert + remove
  *   orc_sq8_*                       SQ8Quantizer (space/quant/sq8.hpp:99-143) and the AVX-512 /
  *                                   AVX2 SQ8 kernels (distance_l2.ipp:244-408, distance_ip.ipp:198-366)
  *
@@ -110,6 +113,18 @@ void orc_rerank(const orc_index *ix, const float *query, const uint32_t *search_
 /* The batch path's rerank loop (index.hpp:337-345), single-threaded over nq queries; returns seconds. */
 double orc_batch_rerank(const orc_index *ix, const float *queries, uint64_t nq, const uint32_t *search_ids,
                         uint32_t k, uint32_t ef, uint32_t *ids, float *dists);
+
+/* ---- online updates ------------------------------------------------------------------------
+ * An updater copies the index (rows, l0, validity, overlay) into growable storage with room for
+ * `capacity` nodes; insert = insert_and_update (search_solo for R ids at ef, append, update every
+ * node that gained an edge), returns the new id or -1 when full; remove = GraphUpdateJob::remove.
+ * orc_updater_view() is the current index (pointers change after an insert). */
+typedef struct orc_updater orc_updater;
+orc_updater *orc_updater_new(const orc_index *ix, uint64_t capacity);
+void orc_updater_free(orc_updater *u);
+const orc_index *orc_updater_view(orc_updater *u);
+int64_t orc_updater_insert(orc_updater *u, const float *search_query, const float *row, uint32_t ef);
+void orc_updater_remove(orc_updater *u, uint32_t id);
 
 /* ---- SQ8 ---------------------------------------------------------------------------------- */
 void orc_sq8_fit(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v);
