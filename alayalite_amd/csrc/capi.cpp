@@ -117,6 +117,8 @@ struct alaya_index {
   // scratch
   DevBuf work, overflow, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
   uint32_t hash_log2_override = 0;
+  int visited_mode_override = 0;  // 0 auto, 1 compact 16-bit slots, 2 wide 32-bit slots,
+                                  // 3 compact with probes capped at 2 (exercises the probe spill)
   int num_cus = 0;
   // online updates (alaya_index_enable_updates): host mirror + JobContext, device capacity
   uint64_t capacity = 0;
@@ -151,7 +153,27 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 // CU (capped by what the register file admits); the table takes what LDS is left per query,
 // never more than ~2x the expected visited count (~24 ids per expansion x ef), never below
 // 1024 slots.  A query that outgrows its table spills to the global bitset (exact either way).
-uint32_t auto_hash_log2(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef) {
+// Layout: compact 16-bit slots (twice the entries per byte) whenever the ids' hash remainder fits
+// (log2 n - log2 slots <= 11), else 32-bit id slots.  Returns log2 slots; sets p.vis_*.
+constexpr uint32_t kMaxCompactRbits = 11;
+
+uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef) {
+  const uint32_t lbits = std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2)));
+  const int mode = ix->visited_mode_override;  // 0 auto, 1 compact, 2 wide, 3 compact + short probes
+  auto set_mode = [&](uint32_t l, bool compact) {
+    p.vis_lbits = lbits;
+    p.vis_rbits = compact ? (lbits > l ? lbits - l : 0u) : alaya_amd::kVisWide;
+    p.vis_max_disp = compact ? (0xffffu >> p.vis_rbits) - 1u : 0u;
+    if (compact && mode == 3) p.vis_max_disp = std::min<uint32_t>(p.vis_max_disp, 2u);
+    return l;
+  };
+  auto fits_compact = [&](uint32_t l) { return (lbits > l ? lbits - l : 0u) <= kMaxCompactRbits; };
+  if (ix->hash_log2_override) {
+    const uint32_t l = ix->hash_log2_override;
+    const bool compact = mode == 1 || mode == 3 || (mode == 0 && fits_compact(l));
+    if (compact && !fits_compact(l)) throw ArgError("compact visited table cannot encode ids of this index");
+    return set_mode(l, compact);
+  }
   const size_t fixed = alaya_amd::search_lds_bytes(ix->stride, ef, 0, p.sq8_order != 0) - 4;
   int vgpr_blocks = 0;
   hip_check(alaya_amd::search_occupancy(p, fixed + 4096, &vgpr_blocks), "occupancy");
@@ -159,9 +181,18 @@ uint32_t auto_hash_log2(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t 
   const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_blocks, want));
   const size_t budget = kLdsPerCu / blocks > fixed ? kLdsPerCu / blocks - fixed : 0;
-  uint32_t l = 10;
-  while (l < 15 && (static_cast<size_t>(4) << (l + 1)) <= budget) ++l;
-  return std::max<uint32_t>(10, std::min<uint32_t>(l, ceil_log2(48ull * ef)));
+  const uint32_t cap = ceil_log2(48ull * ef);
+  auto pick = [&](size_t slot_bytes, uint32_t lmax) {
+    uint32_t l = 10;
+    while (l < lmax && (slot_bytes << (l + 1)) <= budget) ++l;
+    return std::max<uint32_t>(10, std::min<uint32_t>(l, cap));
+  };
+  if (mode != 2) {
+    const uint32_t l = pick(2, 16);
+    if (fits_compact(l)) return set_mode(l, true);
+    if (mode == 1 || mode == 3) throw ArgError("compact visited table cannot encode ids of this index");
+  }
+  return set_mode(pick(4, 15), false);
 }
 
 void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t ef,
@@ -202,8 +233,8 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.sq_max = ix->sq_max.as<float>();
     p.stamps = nullptr;
   }
-  p.hash_log2 = ix->hash_log2_override ? ix->hash_log2_override : auto_hash_log2(ix, p, nq, ef);
-  const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2, sq8);
+  p.hash_log2 = size_visited(ix, p, nq, ef);
+  const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2, sq8, p.vis_rbits != alaya_amd::kVisWide);
   if (lds > 160 * 1024) throw ArgError("ef / dim too large for the LDS budget");
   int per_cu = 0;
   hip_check(alaya_amd::search_occupancy(p, lds, &per_cu), "occupancy");
@@ -1044,8 +1075,16 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots) {
   return guarded([&] {
     if (!ix) throw ArgError("null index");
-    if (log2_slots != 0 && (log2_slots < 6 || log2_slots > 15)) throw ArgError("log2_slots must be 0 or 6..15");
+    if (log2_slots != 0 && (log2_slots < 6 || log2_slots > 16)) throw ArgError("log2_slots must be 0 or 6..16");
     ix->hash_log2_override = log2_slots;
+  });
+}
+
+int alaya_index_set_visited_mode(alaya_index *ix, int mode) {
+  return guarded([&] {
+    if (!ix) throw ArgError("null index");
+    if (mode < 0 || mode > 3) throw ArgError("visited mode must be 0 (auto), 1 (compact), 2 (wide) or 3 (test)");
+    ix->visited_mode_override = mode;
   });
 }
 

@@ -257,6 +257,7 @@ class PyIndexInterface {
     return out;
   }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
+  void set_visited_mode(int m) { check(alaya_index_set_visited_mode(ix_, m)); }
   // SQ8 batch_search rerank: 1 = the reference's PyIndex::rerank (default), 2 = corrected (whole ef pool)
   void set_rerank_mode(int m) {
     if (m != 1 && m != 2) throw std::invalid_argument("rerank mode must be 1 (reference) or 2 (corrected)");
@@ -785,6 +786,7 @@ class DeviceIndex {
                                 reinterpret_cast<void *>(stream)));
   }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
+  void set_visited_mode(int m) { check(alaya_index_set_visited_mode(ix_, m)); }
   py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
                            uint32_t ef) {
     const uint64_t nq = q.shape(0);
@@ -873,6 +875,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("get_data_dim", &PyIndexInterface::get_data_dim)
       .def("last_counters", &PyIndexInterface::last_counters)
       .def("set_hash_log2", &PyIndexInterface::set_hash_log2)
+      .def("set_visited_mode", &PyIndexInterface::set_visited_mode)
       .def("set_rerank_mode", &PyIndexInterface::set_rerank_mode)
       .def("rerank_mode", &PyIndexInterface::rerank_mode)
       .def("device_distances", &PyIndexInterface::device_distances)
@@ -895,6 +898,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("search_device", &DeviceIndex::search_device)
       .def("distances", &DeviceIndex::distances)
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
+      .def("set_visited_mode", &DeviceIndex::set_visited_mode)
       .def("flat_search", &DeviceIndex::flat_search, py::arg("queries"), py::arg("k"))
       .def("flat_search_device", &DeviceIndex::flat_search_device)
       .def("flat_diag", &DeviceIndex::flat_diag)

@@ -42,6 +42,11 @@ struct SearchParams {
   uint32_t *work_counter; // zeroed before each launch
   uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area
   uint32_t hash_log2;     // LDS visited table = 1 << hash_log2 slots
+  // visited-table layout: kVisWide = 32-bit id slots; otherwise 16-bit compact slots holding
+  // (probe distance, low vis_rbits bits of a vis_lbits-bit bijective hash) -- exact either way
+  uint32_t vis_rbits;
+  uint32_t vis_lbits;
+  uint32_t vis_max_disp;  // compact: largest probe distance an entry may sit at (<= 0xffff >> rbits - 1)
   uint64_t *stamps;       // nullable: diagnostic per-phase cycle counts, nq x 8
   // SQ8 search space (SQ8Space, space/sq8_space.hpp): traversal distances on uint8 codes
   int sq8_order;          // 0 = f32 RawSpace search; 2 = AVX-512 SQ8 order; 1 = AVX2 SQ8 order
@@ -61,7 +66,12 @@ struct RerankParams {
   float *out_dists;            // nq x k (nullable)
 };
 
-size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8 = false);
+constexpr uint32_t kVisWide = 0xffffffffu;
+// bytes of the LDS visited table / of the whole per-workgroup LDS footprint
+inline size_t visited_table_bytes(uint32_t hash_log2, bool compact) {
+  return (static_cast<size_t>(compact ? 2 : 4)) << hash_log2;
+}
+size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8 = false, bool compact = false);
 // rerank: p.base/p.queries are the raw f32 rows and the (normalised) f32 queries
 hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream);
 hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu);

@@ -315,7 +315,15 @@ __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds
 }
 
 // --------------------------------------------------------------------------------------------
-// Visited set: exact.  Returns true if v was not yet in the set (and inserts it).
+// Visited set: exact (DynamicBitset semantics, query_utils.hpp:69-115).  First level: an LDS
+// open-addressing table with linear probing.  Two layouts:
+//   wide    -- 32-bit slots holding the id (kEmpty = free);
+//   compact -- 16-bit slots.  h = (v * C) mod 2^L is a bijection on [0, 2^L) (C odd,
+//              L = vis_lbits >= log2 n); the home slot is the top log2h bits of h and the slot
+//              stores 1 + (probe distance << rbits | low rbits bits of h), so (slot, entry)
+//              identifies v exactly in half the bytes: twice the entries per LDS byte.
+// When the table passes its load limit (or a compact probe would exceed the encodable distance)
+// the query spills: a per-slot global N-bit bitset becomes the second level (atomicOr).
 // --------------------------------------------------------------------------------------------
 struct Visited {
   uint32_t *tab;
@@ -324,42 +332,97 @@ struct Visited {
   uint32_t limit;        // switch to the global bitset above this many entries
   bool spilled;          // wave-uniform
   uint32_t *bits;        // per-slot global bitset (valid when spilled)
+  uint32_t rbits;        // compact: remainder bits; kVisWide: 32-bit slots
+  uint32_t lmask;        // compact: 2^L - 1
+  uint32_t lshift;       // compact, L < log2h: home = h << lshift
+  uint32_t max_disp;     // compact: largest encodable probe distance
 };
 
-__device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
-  const uint32_t mask = (1u << vs.log2h) - 1u;
-  uint32_t h = hash_slot(v, vs.log2h);
-  for (;;) {
-    const uint32_t e = vs.tab[h];
-    if (e == v) return true;
-    if (e == kEmpty) return false;
-    h = (h + 1) & mask;
+__device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t *tab, uint32_t *bits) {
+  Visited vs;
+  vs.tab = tab;
+  vs.log2h = p.hash_log2;
+  vs.count = 0u;
+  vs.spilled = false;
+  vs.bits = bits;
+  vs.rbits = p.vis_rbits;
+  const uint32_t hsize = 1u << p.hash_log2;
+  if (p.vis_rbits == kVisWide) {
+    vs.limit = hsize / 2;
+    vs.lmask = vs.lshift = vs.max_disp = 0u;
+  } else {
+    vs.limit = hsize - hsize / 4 - hsize / 16;  // load factor 0.69
+    vs.lmask = p.vis_lbits >= 32 ? 0xffffffffu : (1u << p.vis_lbits) - 1u;
+    vs.lshift = p.vis_lbits < p.hash_log2 ? p.hash_log2 - p.vis_lbits : 0u;
+    vs.max_disp = p.vis_max_disp;
+  }
+  return vs;
+}
+
+__device__ __forceinline__ void compact_key(const Visited &vs, uint32_t v, uint32_t &home, uint32_t &rem) {
+  const uint32_t h = (v * 0x9E3779B1u) & vs.lmask;
+  if (vs.rbits) {
+    home = h >> vs.rbits;
+    rem = h & ((1u << vs.rbits) - 1u);
+  } else {
+    home = h << vs.lshift;
+    rem = 0u;
   }
 }
 
-// All lanes with `act` insert their v; duplicates among lanes must have been removed.
-__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
-  bool fresh = false;
-  if (!vs.spilled) {
-    if (act) {
-      const uint32_t mask = (1u << vs.log2h) - 1u;
-      uint32_t h = hash_slot(v, vs.log2h);
-      for (;;) {
-        const uint32_t old = atomicCAS(&vs.tab[h], kEmpty, v);
-        if (old == kEmpty) { fresh = true; break; }
-        if (old == v) break;
-        h = (h + 1) & mask;
-      }
-    }
-    vs.count += __popcll(ballot(fresh));
-  } else if (act) {
-    if (!table_lookup(vs, v)) {
-      const uint32_t bit = 1u << (v & 31);
-      const uint32_t old = atomicOr(&vs.bits[v >> 5], bit);
-      fresh = (old & bit) == 0u;
+__device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
+  const uint32_t mask = (1u << vs.log2h) - 1u;
+  if (vs.rbits == kVisWide) {
+    uint32_t h = hash_slot(v, vs.log2h);
+    for (;;) {
+      const uint32_t e = vs.tab[h];
+      if (e == v) return true;
+      if (e == kEmpty) return false;
+      h = (h + 1) & mask;
     }
   }
-  return fresh;
+  uint32_t home, rem;
+  compact_key(vs, v, home, rem);
+  const uint16_t *t16 = reinterpret_cast<const uint16_t *>(vs.tab);
+  for (uint32_t i = 0;; ++i) {
+    const uint32_t e = t16[(home + i) & mask];
+    if (e == 0u) return false;
+    if (e == 1u + ((i << vs.rbits) | rem)) return true;
+    if (i == vs.max_disp) return false;  // inserts never go further
+  }
+}
+
+// Insert into the LDS table.  Returns 1 = inserted (fresh), 0 = already present, 2 = compact probe
+// ran past max_disp (not present, not inserted: the caller spills).
+__device__ __forceinline__ int table_insert(const Visited &vs, uint32_t v) {
+  const uint32_t mask = (1u << vs.log2h) - 1u;
+  if (vs.rbits == kVisWide) {
+    uint32_t h = hash_slot(v, vs.log2h);
+    for (;;) {
+      const uint32_t old = atomicCAS(&vs.tab[h], kEmpty, v);
+      if (old == kEmpty) return 1;
+      if (old == v) return 0;
+      h = (h + 1) & mask;
+    }
+  }
+  uint32_t home, rem;
+  compact_key(vs, v, home, rem);
+  for (uint32_t i = 0; i <= vs.max_disp; ++i) {
+    const uint32_t slot = (home + i) & mask;
+    uint32_t *w = &vs.tab[slot >> 1];
+    const uint32_t sh = (slot & 1u) * 16u;
+    const uint32_t mine = 1u + ((i << vs.rbits) | rem);
+    uint32_t cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+      const uint32_t e = (cur >> sh) & 0xffffu;
+      if (e == mine) return 0;
+      if (e != 0u) break;  // occupied by another key: next slot
+      const uint32_t old = atomicCAS(w, cur, cur | (mine << sh));
+      if (old == cur) return 1;
+      cur = old;  // the other half of the word (or this slot) changed: re-examine
+    }
+  }
+  return 2;
 }
 
 __device__ void spill_begin(Visited &vs, uint64_t n_words) {
@@ -369,6 +432,30 @@ __device__ void spill_begin(Visited &vs, uint64_t n_words) {
   __threadfence_block();
   wave_sync();
   vs.spilled = true;
+}
+
+__device__ __forceinline__ bool global_visit(const Visited &vs, uint32_t v) {
+  const uint32_t bit = 1u << (v & 31);
+  const uint32_t old = atomicOr(&vs.bits[v >> 5], bit);
+  return (old & bit) == 0u;
+}
+
+// All lanes with `act` insert their v; duplicates among lanes must have been removed.
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, uint64_t n_words) {
+  bool fresh = false;
+  if (!vs.spilled) {
+    int r = 0;
+    if (act) r = table_insert(vs, v);
+    fresh = r == 1;
+    vs.count += __popcll(ballot(fresh));
+    if (ballot(r == 2)) {  // a compact probe ran out of encodable distance: spill now
+      spill_begin(vs, n_words);
+      if (r == 2) fresh = global_visit(vs, v);
+    }
+  } else if (act) {
+    if (!table_lookup(vs, v)) fresh = global_visit(vs, v);
+  }
+  return fresh;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -500,7 +587,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     L.pi = reinterpret_cast<uint32_t *>(ptr);
     ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
     L.hash = reinterpret_cast<uint32_t *>(ptr);
-    ptr += (static_cast<size_t>(1) << p.hash_log2) * 4;
+    ptr += static_cast<size_t>(p.vis_rbits != kVisWide ? 2 : 4) << p.hash_log2;
     L.sq_scale = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
     ptr += kSpace ? static_cast<size_t>(p.stride) * 4 : 0;
     L.sq_min = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
@@ -553,13 +640,17 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
         L.sq_min[e] = mn;
       }
     }
-    for (uint32_t e = lane; e < hsize; e += 64) L.hash[e] = kEmpty;
+    {
+      const bool wide = p.vis_rbits == kVisWide;
+      const uint32_t words = wide ? hsize : hsize / 2;
+      for (uint32_t e = lane; e < words; e += 64) L.hash[e] = wide ? kEmpty : 0u;
+    }
     for (uint32_t e = lane; e <= p.ef; e += 64) {
       L.pd[e] = 0.f;
       L.pi[e] = 0u;
     }
     wave_sync();
-    Visited vs{L.hash, p.hash_log2, 0u, hsize / 2, false, slot_bits};
+    Visited vs = make_visited(p, L.hash, slot_bits);
     PoolState ps{0u, 0u, p.ef};
     uint32_t n_dist = 0, n_expand = 0, n_dist_up = 0, n_hops_up = 0;
 
@@ -610,7 +701,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       }
       ps.size = 1;
       ps.cur = 0;
-      visit(vs, u, lane == 0);
+      visit(vs, u, lane == 0, bit_words);
       wave_sync();
     } else {
       // NSG-style entry points: insert each ep, then mark it visited (graph.hpp:153-156)
@@ -631,7 +722,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
         for (uint32_t j = 0; j < cnt; ++j) {
           const uint32_t vj = __shfl(v, j);
           if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
-          visit(vs, vj, lane == 0);
+          visit(vs, vj, lane == 0, bit_words);
         }
         wave_sync();
       }
@@ -667,7 +758,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
         }
       }
       if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
-      const bool fresh = visit(vs, v, act);
+      const bool fresh = visit(vs, v, act, bit_words);
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
       stamp(2);
@@ -804,9 +895,9 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
 }
 }  // namespace
 
-size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8) {
+size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8, bool compact) {
   return static_cast<size_t>(stride) * 4 + 3 * 64 * 4 + 2 * (((ef + 1) * 4 + 15) / 16 * 16) +
-         (static_cast<size_t>(1) << hash_log2) * 4 + (sq8 ? 2 * static_cast<size_t>(stride) * 4 : 0);
+         visited_table_bytes(hash_log2, compact) + (sq8 ? 2 * static_cast<size_t>(stride) * 4 : 0);
 }
 
 hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream) {

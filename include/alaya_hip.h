@@ -155,8 +155,12 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
                             uint32_t *ids, float *dists, uint32_t *n_recomputed);
 int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
                                    uint32_t *d_ids, float *d_dists, uint32_t *d_flags, void *stream);
-/* Tuning / introspection: LDS visited-table size (log2 slots; 0 = automatic). */
+/* Tuning / introspection: LDS visited-table size (log2 slots, 6..16; 0 = automatic) and layout
+ * (0 = automatic, 1 = compact 16-bit slots, 2 = 32-bit id slots, 3 = compact with probe distance
+ * capped at 2, a test hook for the spill-on-long-probe path).  Results never depend on either:
+ * the visited set is exact (DynamicBitset, include/utils/query_utils.hpp:69-115). */
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots);
+int alaya_index_set_visited_mode(alaya_index *ix, int mode);
 int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,
                      int *metric, uint64_t *device_bytes);
 

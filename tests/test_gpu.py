@@ -76,14 +76,33 @@ def test_k_larger_than_ef(native, orc, c1):
         assert not ids[i, 5:].any() and not dists[i, 5:].any()
 
 
-@pytest.mark.parametrize("log2", [6, 8, 11])
-def test_visited_spill_path(native, orc, c1, log2):
-    """Tiny LDS tables force the per-slot global bitset; results must not change."""
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("log2", [6, 8, 11, 14])
+def test_visited_spill_path(native, orc, c1, log2, mode):
+    """Visited-table layouts (1 compact 16-bit, 2 wide 32-bit, 3 compact with probes capped at 2)
+    at sizes from tiny (immediate spill to the per-slot global bitset) to roomy (no spill, and for
+    C1's n=1000 ids narrower than the table); results must not change."""
     base, queries = c1
     g, view = _graph_view(native, orc, base)
     dev = _dev(native, base, g)
     dev.set_hash_log2(log2)
+    dev.set_visited_mode(mode)
     _check(view, dev, queries, 10, 100)
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_visited_compact_wide_remainder(native, orc, mode):
+    """Compact layout with many remainder bits (n = 70k ids, 2^6..2^9 slots: rbits 8..11, the
+    largest encodable), so entries carry short probe distances; results must not change."""
+    rng = np.random.default_rng(21)
+    base = rng.random((70000, 16), dtype=np.float32)
+    queries = rng.random((16, 16), dtype=np.float32)
+    g, view = _graph_view(native, orc, base, threads=8)
+    for log2 in (6, 9):
+        dev = _dev(native, base, g)
+        dev.set_hash_log2(log2)
+        dev.set_visited_mode(mode)
+        _check(view, dev, queries, 10, 200)
 
 
 @pytest.mark.parametrize("metric", [1, 2])
