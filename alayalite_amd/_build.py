@@ -25,8 +25,8 @@ ARCH = os.environ.get("ALAYA_OFFLOAD_ARCH", "gfx950")
 LIB = os.path.join(HERE, "libalaya_hip.so")
 EXT = os.path.join(HERE, "_alayalitepy" + sysconfig.get_config_var("EXT_SUFFIX"))
 
-LIB_SOURCES = ["search_kernels.hip", "flat_kernels.hip", "capi.cpp", "hnsw_build.cpp", "graph_update.cpp"]
-LIB_HEADERS = ["search_kernels.h", "flat_kernels.h", "hnsw_build.h", "host_distance.h", "graph_update.h"]
+LIB_SOURCES = ["search_kernels.hip", "build_kernels.hip", "flat_kernels.hip", "capi.cpp", "hnsw_build.cpp", "graph_update.cpp"]
+LIB_HEADERS = ["search_kernels.h", "search_device.h", "build_kernels.h", "flat_kernels.h", "hnsw_build.h", "host_distance.h", "graph_update.h"]
 EXT_SOURCES = ["pybind_module.cpp"]
 
 

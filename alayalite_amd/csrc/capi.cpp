@@ -14,6 +14,7 @@
 #include <thread>
 #include <vector>
 
+#include "build_kernels.h"
 #include "graph_update.h"
 #include "hnsw_build.h"
 #include "flat_kernels.h"
@@ -747,6 +748,257 @@ int alaya_index_export_rows(alaya_index *ix, float *rows, uint8_t *valid_bitmap,
     *n = ix->upd_graph->n;
     if (rows) std::memcpy(rows, ix->upd_rows->rows.data(), ix->upd_rows->rows.size() * 4);
     if (valid_bitmap) std::memcpy(valid_bitmap, ix->upd_rows->valid.data(), (*n + 7) / 8);
+  });
+}
+
+}  // extern "C"
+
+// ---- device graph construction ----------------------------------------------------------------
+namespace {
+
+// One launch group of the batched build: the points of batch [first, ...) active at `level`.
+struct BuildStep {
+  uint32_t first;
+  int level;
+  int max_level;  // graph max level before the batch
+  uint32_t ep;    // graph entry point before the batch
+  uint64_t off;   // active points: act[off, off + cnt)
+  uint32_t cnt;
+  int refine;     // level-0 refine pass of the batch
+};
+
+// Batch schedule (label order): batch size max(1, min(max_batch, inserted / batch_div)); a point
+// whose level exceeds the graph's max level closes its batch, so the entry point / max level a
+// batch sees are exactly the sequential ones (hnswlib.hpp:740-748).
+std::vector<BuildStep> build_schedule(const std::vector<uint32_t> &lv, uint32_t batch_div, uint32_t max_batch,
+                                      uint32_t refine, std::vector<uint32_t> &act, uint32_t *final_ep,
+                                      int *final_max) {
+  std::vector<BuildStep> steps;
+  const uint64_t n = lv.size();
+  uint32_t ep = 0;
+  int maxl = n ? static_cast<int>(lv[0]) : 0;
+  uint64_t i = 1;
+  while (i < n) {
+    const uint64_t b = std::max<uint64_t>(1, std::min<uint64_t>(max_batch, i / batch_div));
+    uint64_t end = std::min<uint64_t>(n, i + b);
+    int top = 0;
+    for (uint64_t j = i; j < end; ++j) {
+      top = std::max(top, std::min(static_cast<int>(lv[j]), maxl));
+      if (static_cast<int>(lv[j]) > maxl) {
+        end = j + 1;
+        break;
+      }
+    }
+    for (int L = top; L >= 0; --L) {
+      BuildStep st{static_cast<uint32_t>(i), L, maxl, ep, act.size(), 0, 0};
+      for (uint64_t j = i; j < end; ++j)
+        if (std::min(static_cast<int>(lv[j]), maxl) >= L) act.push_back(static_cast<uint32_t>(j));
+      st.cnt = static_cast<uint32_t>(act.size() - st.off);
+      steps.push_back(st);
+    }
+    // refine passes over level 0 (single-point batches have no batch mates to find)
+    for (uint32_t r = 0; r < refine && end - i > 1; ++r) {
+      BuildStep st = steps.back();
+      st.refine = 1;
+      steps.push_back(st);
+    }
+    if (static_cast<int>(lv[end - 1]) > maxl) {
+      ep = static_cast<uint32_t>(end - 1);
+      maxl = static_cast<int>(lv[end - 1]);
+    }
+    i = end;
+  }
+  *final_ep = ep;
+  *final_max = maxl;
+  return steps;
+}
+
+}  // namespace
+
+extern "C" {
+
+int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_construction, uint64_t seed,
+                            uint32_t batch_div, uint32_t max_batch, uint32_t refine, alaya_graph **out,
+                            uint64_t *stats) {
+  return guarded([&] {
+    if (!ix) throw ArgError("invalid arguments");
+    if (R < 2 || R > 64 || R % 2) throw ArgError("max_nbrs must be even and in 2..64 for the device build");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    if (!ix->base.ptr || ix->n == 0) throw ArgError("index has no base vectors");
+    if (ix->n >= (1ull << 31)) throw ArgError("ids must stay below 2^31 (LinearPool checked bit)");
+    const uint64_t n = ix->n;
+    const uint32_t M = R / 2;                            // hnsw_builder.hpp:71-72: M = R/2, M0 = R
+    const uint32_t ef = std::max(ef_construction, M);    // hnswlib.hpp:104
+    batch_div = batch_div ? batch_div : 16;
+    max_batch = max_batch ? max_batch : 65536;
+    hipStream_t st = ix->stream;
+    hipEvent_t e0, e1;
+    hip_check(hipEventCreate(&e0), "event");
+    hip_check(hipEventCreate(&e1), "event");
+
+    // levels and overlay offsets are known up front (upper lists R wide, HNSWBuilder's export)
+    const std::vector<uint32_t> lv = alaya_amd::hnsw_levels(n, M, seed);
+    std::vector<uint64_t> off(n);
+    uint64_t n_upper = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      off[i] = n_upper;
+      n_upper += static_cast<uint64_t>(lv[i]) * R;
+    }
+    std::vector<uint32_t> act;
+    uint32_t ep = 0;
+    int maxl = 0;
+    const std::vector<BuildStep> steps = build_schedule(lv, batch_div, max_batch, refine, act, &ep, &maxl);
+    uint32_t bmax = 1;
+    for (const BuildStep &s : steps) bmax = std::max(bmax, s.cnt);
+
+    // device graph (installed as the index's search graph) + scratch
+    ix->has_graph = false;
+    ix->upd_graph.reset();
+    ix->upd_rows.reset();
+    ix->upd_ctx.reset();
+    ix->l0.release();
+    ix->l0.reserve(n * R * 4);
+    ix->levels.release();
+    ix->levels.reserve(n * 4);
+    ix->upper_off.release();
+    ix->upper_off.reserve(n * 8);
+    ix->upper_edges.release();
+    ix->upper_edges.reserve(std::max<uint64_t>(n_upper, 1) * 4);
+    hip_check(hipMemsetAsync(ix->l0.ptr, 0xff, n * R * 4, st), "memset");
+    if (n_upper) hip_check(hipMemsetAsync(ix->upper_edges.ptr, 0xff, n_upper * 4, st), "memset");
+    hip_check(hipMemcpyAsync(ix->levels.ptr, lv.data(), n * 4, hipMemcpyHostToDevice, st), "H2D");
+    hip_check(hipMemcpyAsync(ix->upper_off.ptr, off.data(), n * 8, hipMemcpyHostToDevice, st), "H2D");
+    DevBuf d_act, d_next, c_ids, c_d, c_n, k_in, k_out, dd_in, dd_out, sort_tmp, cnt;
+    d_act.reserve(std::max<size_t>(act.size(), 1) * 4);
+    if (!act.empty())
+      hip_check(hipMemcpyAsync(d_act.ptr, act.data(), act.size() * 4, hipMemcpyHostToDevice, st), "H2D");
+    d_next.reserve(static_cast<size_t>(max_batch) * 4);
+    c_ids.reserve(static_cast<size_t>(bmax) * ef * 4);
+    c_d.reserve(static_cast<size_t>(bmax) * ef * 4);
+    c_n.reserve(static_cast<size_t>(bmax) * 4);
+    const size_t n_edge_max = static_cast<size_t>(bmax) * M;
+    k_in.reserve(n_edge_max * 8);
+    k_out.reserve(n_edge_max * 8);
+    dd_in.reserve(n_edge_max * 4);
+    dd_out.reserve(n_edge_max * 4);
+    size_t tmp_bytes = 0;
+    hip_check(alaya_amd::sort_edges(nullptr, &tmp_bytes, nullptr, nullptr, nullptr, nullptr, n_edge_max, st), "sort size");
+    sort_tmp.reserve(tmp_bytes);
+    cnt.reserve(8 * 4);
+    hip_check(hipMemsetAsync(cnt.ptr, 0, 8 * 4, st), "memset");
+    ix->work.reserve(4);
+
+    alaya_amd::BuildParams bp{};
+    bp.s = base_params(ix);
+    bp.s.valid = nullptr;
+    bp.s.l0 = ix->l0.as<uint32_t>();
+    bp.s.R = R;
+    bp.s.levels = ix->levels.as<uint32_t>();
+    bp.s.upper_off = ix->upper_off.as<uint64_t>();
+    bp.s.upper_edges = ix->upper_edges.as<uint32_t>();
+    bp.s.upper_R = R;
+    bp.s.queries = nullptr;
+    bp.s.ef = ef;
+    bp.s.work_counter = ix->work.as<uint32_t>();
+    bp.l0w = ix->l0.as<uint32_t>();
+    bp.upw = ix->upper_edges.as<uint32_t>();
+    bp.next = d_next.as<uint32_t>();
+    bp.cand_ids = c_ids.as<uint32_t>();
+    bp.cand_d = c_d.as<float>();
+    bp.cand_n = c_n.as<uint32_t>();
+    bp.M = M;
+    bp.counters = cnt.as<uint32_t>();
+    // visited-set sizing and the spill area for the largest batch (sized once: kernels in flight)
+    {
+      SearchParams probe = bp.s;
+      const uint32_t hl = size_visited(ix, probe, bmax, ef);
+      const size_t lds = alaya_amd::build_lds_bytes(ix->stride, ef, hl, probe.vis_rbits != alaya_amd::kVisWide);
+      bp.s.hash_log2 = hl;
+      bp.s.vis_rbits = probe.vis_rbits;
+      bp.s.vis_lbits = probe.vis_lbits;
+      bp.s.vis_max_disp = probe.vis_max_disp;
+      if (lds > kLdsPerCu) throw ArgError("ef_construction / dim too large for the LDS budget");
+    }
+    const size_t lds = alaya_amd::build_lds_bytes(ix->stride, ef, bp.s.hash_log2, bp.s.vis_rbits != alaya_amd::kVisWide);
+    int per_cu = 0;
+    hip_check(alaya_amd::build_search_occupancy(bp, lds, &per_cu), "occupancy");
+    per_cu = std::max(1, per_cu);
+    const uint64_t grid_max = static_cast<uint64_t>(per_cu) * ix->num_cus;
+    const uint64_t words = (n + 31) / 32;
+    ix->overflow.reserve(static_cast<size_t>(std::min<uint64_t>(grid_max, bmax)) * words * 4);
+    bp.s.overflow_bits = ix->overflow.as<uint32_t>();
+
+    hip_check(hipEventRecord(e0, st), "event");
+    uint64_t launches = 0;
+    for (const BuildStep &s : steps) {
+      bp.s.nq = s.cnt;
+      bp.s.ep = s.ep;
+      bp.pts = d_act.as<uint32_t>() + s.off;
+      bp.batch_first = s.first;
+      bp.level = s.level;
+      bp.max_level = s.max_level;
+      bp.refine = s.refine;
+      bp.Mmax = s.level == 0 ? R : M;
+      bp.edge_keys = k_in.as<uint64_t>();
+      bp.edge_d = dd_in.as<float>();
+      const int grid = static_cast<int>(std::min<uint64_t>(s.cnt, grid_max));
+      const int wide = static_cast<int>(std::min<uint64_t>(s.cnt, static_cast<uint64_t>(ix->num_cus) * 16));
+      hip_check(hipMemsetAsync(bp.s.work_counter, 0, 4, st), "memset");
+      hip_check(alaya_amd::launch_build_search(bp, grid, lds, st), "build search");
+      hip_check(alaya_amd::launch_build_select(bp, wide, st), "build select");
+      const uint64_t ne = static_cast<uint64_t>(s.cnt) * M;
+      size_t tb = tmp_bytes;
+      hip_check(alaya_amd::sort_edges(sort_tmp.ptr, &tb, k_in.as<uint64_t>(), k_out.as<uint64_t>(), dd_in.as<float>(),
+                                      dd_out.as<float>(), ne, st), "sort edges");
+      bp.edge_keys = k_out.as<uint64_t>();
+      bp.edge_d = dd_out.as<float>();
+      bp.n_edges = ne;
+      const int agrid = static_cast<int>(std::min<uint64_t>((ne + 63) / 64, static_cast<uint64_t>(ix->num_cus) * 16));
+      hip_check(alaya_amd::launch_build_apply(bp, agrid, st), "build apply");
+      launches += 4;
+    }
+    hip_check(hipEventRecord(e1, st), "event");
+    HostGraph g;
+    g.n = n;
+    g.R = R;
+    g.l0.resize(n * R);
+    g.has_overlay = true;
+    g.upper_R = R;
+    g.ep = ep;
+    g.levels = lv;
+    g.upper_off = off;
+    g.upper_edges.resize(n_upper);
+    hip_check(hipMemcpyAsync(g.l0.data(), ix->l0.ptr, n * R * 4, hipMemcpyDeviceToHost, st), "D2H");
+    if (n_upper)
+      hip_check(hipMemcpyAsync(g.upper_edges.data(), ix->upper_edges.ptr, n_upper * 4, hipMemcpyDeviceToHost, st), "D2H");
+    uint32_t hc[8] = {0};
+    hip_check(hipMemcpyAsync(hc, cnt.ptr, sizeof(hc), hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "device build");
+    float ms = 0.f;
+    hip_check(hipEventElapsedTime(&ms, e0, e1), "event");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    ix->R = R;
+    ix->upper_R = R;
+    ix->ep = ep;
+    ix->n_eps = 0;
+    ix->has_overlay = true;
+    ix->dedup = false;
+    ix->graph_n = n;
+    ix->has_graph = true;
+    if (stats) {
+      stats[0] = steps.empty() ? 0 : 1;
+      for (size_t i = 1; i < steps.size(); ++i) stats[0] += steps[i].first != steps[i - 1].first ? 1 : 0;
+      stats[1] = launches;
+      stats[2] = hc[0];
+      stats[3] = hc[1];
+      stats[4] = hc[2];
+      stats[5] = static_cast<uint64_t>(ms * 1000.0);
+      stats[6] = bmax;
+      stats[7] = static_cast<uint64_t>(maxl);
+    }
+    if (out) *out = new alaya_graph{std::move(g)};
   });
 }
 

@@ -23,6 +23,21 @@ uint32_t HostGraph::max_level() const {
   return has_overlay && !levels.empty() ? levels[ep] : 0;
 }
 
+std::vector<uint32_t> hnsw_levels(uint64_t n, uint32_t M, uint64_t seed) {
+  // Levels are drawn in label order exactly as sequential add_point(0..n-1) draws them
+  // (get_random_level, hnswlib.hpp:182-186; mult_ = 1/ln(M), :118).
+  std::vector<uint32_t> levels(n);
+  std::default_random_engine gen;
+  gen.seed(seed);
+  const double mult = 1.0 / std::log(1.0 * M);
+  for (uint64_t i = 0; i < n; ++i) {
+    std::uniform_real_distribution<double> distribution(0.0, 1.0);
+    double r = -std::log(distribution(gen)) * mult;
+    levels[i] = static_cast<uint32_t>(static_cast<size_t>(r));
+  }
+  return levels;
+}
+
 namespace {
 
 using DistId = std::pair<float, uint32_t>;
@@ -38,16 +53,8 @@ class Builder {
       : data_(data), n_(n), dim_(dim), metric_(metric), M_(M), M0_(2 * M),
         efc_(std::max<size_t>(efc, M)), locks_(n), levels_(n, 0), links0_(n * (1 + 2 * M), 0),
         upper_(n) {
-    // Levels are drawn in label order exactly as sequential add_point(0..n-1) draws them
-    // (get_random_level, hnswlib.hpp:182-186; mult_ = 1/ln(M), :118).
-    std::default_random_engine gen;
-    gen.seed(seed);
-    const double mult = 1.0 / std::log(1.0 * M_);
-    for (uint64_t i = 0; i < n_; ++i) {
-      std::uniform_real_distribution<double> distribution(0.0, 1.0);
-      double r = -std::log(distribution(gen)) * mult;
-      levels_[i] = static_cast<int>(static_cast<size_t>(r));
-    }
+    const std::vector<uint32_t> lv = hnsw_levels(n_, static_cast<uint32_t>(M_), seed);
+    for (uint64_t i = 0; i < n_; ++i) levels_[i] = static_cast<int>(lv[i]);
   }
 
   // The reference holds the new node's lock for the whole insertion (hnswlib.hpp:670); here every

@@ -38,6 +38,10 @@ struct HostGraph {
 HostGraph build_hnsw(const float *data, uint64_t n, uint32_t dim, int metric, uint32_t R,
                      uint32_t ef_construction, uint32_t num_threads, uint64_t seed);
 
+// Per-node top levels in label order: std::default_random_engine seeded with `seed`, level =
+// floor(-ln(U[0,1)) / ln(M)) (get_random_level, hnswlib.hpp:182-186).
+std::vector<uint32_t> hnsw_levels(uint64_t n, uint32_t M, uint64_t seed);
+
 // Reference on-disk format (graph.hpp:165-238 + overlay_graph.hpp:151-194 +
 // sequential_storage.hpp:110-142), IDType = uint32 or uint64 (id_bytes 4 or 8).
 void save_graph(const HostGraph &g, const std::string &path, int id_bytes, uint64_t capacity);

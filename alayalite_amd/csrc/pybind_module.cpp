@@ -116,7 +116,10 @@ class PyIndexInterface {
   std::string to_string() const { return "PyIndexInterface"; }
 
   // PyIndex::fit (index.hpp:177-227)
-  void fit(py::array vectors, uint32_t ef_construction, uint32_t num_threads) {
+  // builder: "host" = HNSWBuilder restated on the host (num_threads == 1 reproduces the reference's
+  // sequential graph exactly); "gpu" = batched insertion on the device (alaya_index_build_graph).
+  void fit(py::array vectors, uint32_t ef_construction, uint32_t num_threads, const std::string &builder) {
+    if (builder != "host" && builder != "gpu") throw py::value_error("builder must be 'host' or 'gpu'");
     if (vectors.ndim() != 2) throw std::runtime_error("Array must be 2D");
     check_dtype(vectors);
     py::array arr = py::array::ensure(vectors, py::array::c_style);
@@ -136,6 +139,20 @@ class PyIndexInterface {
     to_float(raw_.data(), dtype_, n * dim_, rows_f32_.data());
     if (graph_) alaya_graph_free(graph_);
     graph_ = nullptr;
+    if (builder == "gpu") {
+      {
+        py::gil_scoped_release nogil;
+        check(alaya_index_set_base(ix_, rows_f32_.data(), n, dim_, metric_code(), nullptr));
+        check(alaya_index_build_graph(ix_, params_.max_nbrs_, ef_construction, 100, 0, 0, 1, &graph_, nullptr));
+      }
+      if (params_.quantization_type_ == QuantizationType::SQ8) {
+        train_sq8(num_threads);
+        check(alaya_index_set_sq8(ix_, sq_codes_.data(), n_, dim_, sq_min_.data(), sq_max_.data(), host_sq8_order()));
+      }
+      updates_enabled_ = false;
+      graph_dirty_ = false;
+      return;
+    }
     {
       py::gil_scoped_release nogil;
       check(alaya_graph_build_hnsw(rows_f32_.data(), n, dim_, metric_code(), params_.max_nbrs_,
@@ -699,6 +716,26 @@ class DeviceIndex {
     check(alaya_index_set_base(ix_, ptr, n, d, metric, vp));
   }
   void set_graph(const Graph &g) { check(alaya_index_set_graph(ix_, g.get())); }
+  // device HNSW build from the rows set by set_base; the graph becomes this index's search graph
+  py::tuple build_graph(uint32_t R, uint32_t efc, uint64_t seed, uint32_t batch_div, uint32_t max_batch,
+                        uint32_t refine) {
+    alaya_graph *g = nullptr;
+    uint64_t st[8] = {0};
+    {
+      py::gil_scoped_release nogil;
+      check(alaya_index_build_graph(ix_, R, efc, seed, batch_div, max_batch, refine, &g, st));
+    }
+    py::dict stats;
+    stats["batches"] = st[0];
+    stats["launches"] = st[1];
+    stats["prunes"] = st[2];
+    stats["appends"] = st[3];
+    stats["heuristic_dists"] = st[4];
+    stats["device_ms"] = static_cast<double>(st[5]) / 1000.0;
+    stats["max_batch"] = st[6];
+    stats["max_level"] = st[7];
+    return py::make_tuple(std::make_shared<Graph>(g), stats);
+  }
   py::tuple search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k, uint32_t ef) {
     const uint64_t nq = q.shape(0);
     py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
@@ -859,7 +896,8 @@ PYBIND11_MODULE(_alayalitepy, m) {
   py::class_<PyIndexInterface, std::shared_ptr<PyIndexInterface>>(m, "PyIndexInterface")
       .def(py::init<IndexParams>(), py::arg("params"))
       .def("to_string", &PyIndexInterface::to_string)
-      .def("fit", &PyIndexInterface::fit, py::arg("vectors"), py::arg("ef_construction"), py::arg("num_threads"))
+      .def("fit", &PyIndexInterface::fit, py::arg("vectors"), py::arg("ef_construction"), py::arg("num_threads"),
+           py::arg("builder") = "host")
       .def("search", &PyIndexInterface::search, py::arg("query"), py::arg("topk"), py::arg("ef"))
       .def("get_data_by_id", &PyIndexInterface::get_data_by_id, py::arg("id"))
       .def("insert", &PyIndexInterface::insert, py::arg("insert_data"), py::arg("ef"))
@@ -894,6 +932,8 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def(py::init<int>(), py::arg("device") = 0)
       .def("set_base", &DeviceIndex::set_base, py::arg("rows"), py::arg("metric") = 0, py::arg("valid") = py::none())
       .def("set_graph", &DeviceIndex::set_graph)
+      .def("build_graph", &DeviceIndex::build_graph, py::arg("R") = 32, py::arg("ef_construction") = 100,
+           py::arg("seed") = 100, py::arg("batch_div") = 0, py::arg("max_batch") = 0, py::arg("refine") = 1)
       .def("search", &DeviceIndex::search, py::arg("queries"), py::arg("k"), py::arg("ef"))
       .def("search_device", &DeviceIndex::search_device)
       .def("distances", &DeviceIndex::distances)

@@ -1,0 +1,553 @@
+// Device-side building blocks shared by the search kernels (search_kernels.hip) and the graph
+// construction kernels (build_kernels.hip): the bit-exact row distances, the exact visited set and
+// the LinearPool-equivalent candidate pool.  Everything lives in an anonymous namespace, so each
+// translation unit gets its own copy (no relocatable device code).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "search_kernels.h"
+
+namespace alaya_amd {
+namespace {
+
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr uint32_t kChecked = 0x80000000u;
+constexpr uint32_t kIdMask = 0x7fffffffu;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_sync() {
+  // One workgroup == one wave.  LDS instructions of a wave execute in order, so a lane's ds_write
+  // is seen by a later ds_read of any lane; this fence only stops the compiler from reordering LDS
+  // accesses across it and, unlike __syncthreads(), does not drain outstanding global loads.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t v, uint32_t log2h) {
+  return (v * 0x9E3779B1u) >> (32 - log2h);
+}
+
+struct Lds {
+  float *q;          // stride floats
+  float *pd;         // ef + 1 pool distances
+  uint32_t *pi;      // ef + 1 pool ids (bit 31 = checked)
+  uint32_t *hash;    // 1 << hash_log2 visited slots
+  uint32_t *cid;     // 64 candidate ids (adjacency order)
+  float *cd;         // 64 candidate distances
+  float *sd;         // 64 sorted accepted distances
+  float *sq_scale;   // SQ8: per-dimension scale (nullptr for f32 search)
+  float *sq_min;     // SQ8: per-dimension min
+};
+
+// Distance of the query to candidate rows in the index's search space.
+template <bool kIP, int kChunks, int kSpace>
+__device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
+                                                const uint32_t *ids, int n, float *out);
+
+template <bool kIP>
+__device__ __forceinline__ void accumulate(const float4 x, const float4 y, float &a0, float &a1,
+                                           float &a2, float &a3) {
+  if (kIP) {  // acc = fma(x, y, acc)              (distance_ip.ipp:82-85)
+    a0 = fmaf(x.x, y.x, a0); a1 = fmaf(x.y, y.y, a1);
+    a2 = fmaf(x.z, y.z, a2); a3 = fmaf(x.w, y.w, a3);
+  } else {    // diff = x - y; acc = fma(diff, diff, acc)  (distance_l2.ipp:74-83)
+    const float d0 = x.x - y.x, d1 = x.y - y.y, d2 = x.z - y.z, d3 = x.w - y.w;
+    a0 = fmaf(d0, d0, a0); a1 = fmaf(d1, d1, a1);
+    a2 = fmaf(d2, d2, a2); a3 = fmaf(d3, d3, a3);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Distance of the query (LDS) to `n` rows listed in ids[0..n) -> out[0..n).
+// 8 lanes per row (lane m of the group owns partial sums acc[4m..4m+3]); each lane group of a
+// pass handles kRPL rows, so one pass covers 8*kRPL rows and issues every 128 B row chunk of
+// the pass before the first FMA (all loads of the pass in flight at once).
+// --------------------------------------------------------------------------------------------
+template <bool kIP>
+__device__ __forceinline__ float finish_row(float a0, float a1, float a2, float a3) {
+  // (acc0+acc1) + (acc2+acc3) per lane of the 8-wide vector: lanes m^2 then m^4.
+  a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
+  a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+  // lane m==0 holds v[0..3], lane m==1 holds v[4..7]: s[j] = v[j] + v[j+4]; r = (s0+s1)+(s2+s3)
+  const float s0 = a0 + __shfl_xor(a0, 1), s1 = a1 + __shfl_xor(a1, 1);
+  const float s2 = a2 + __shfl_xor(a2, 1), s3 = a3 + __shfl_xor(a3, 1);
+  return (s0 + s1) + (s2 + s3);
+}
+
+template <bool kIP>
+__device__ __forceinline__ float finish_tail(const SearchParams &p, const float *q, const float *row,
+                                             int tail_begin, float res, uint32_t id) {
+  for (int e = tail_begin; e < static_cast<int>(p.dim); ++e) {
+    if (kIP) {
+      res = fmaf(q[e], row[e], res);
+    } else {
+      const float d = q[e] - row[e];
+      res = fmaf(d, d, res);
+    }
+  }
+  if (kIP) res = -res;
+  if (p.valid != nullptr && !((p.valid[id >> 5] >> (id & 31)) & 1u)) res = FLT_MAX;
+  return res;
+}
+
+// rows per lane group per pass for a compile-time chunk count: keep the hoisted row chunks
+// within ~96 float4 (384 VGPRs) -- one wave per SIMD has the whole 512-entry register file.
+template <int kChunks>
+constexpr int rows_per_group() {
+  return kChunks <= 0 ? 1 : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
+}
+
+template <bool kIP, int kChunks>
+__device__ __forceinline__ void row_distances(const SearchParams &p, const float *q,
+                                              const uint32_t *ids, int n, float *out) {
+  const int lane = lane_id();
+  const int g = lane >> 3, m = lane & 7;
+  const int T = kChunks > 0 ? kChunks : static_cast<int>(p.dim >> 5);
+  const int rem = static_cast<int>(p.dim) - 32 * T;
+  const int nb8 = rem >> 3;
+  const int tail_begin = 32 * T + 8 * nb8;
+  if constexpr (kChunks > 0) {
+    constexpr int kRPL = rows_per_group<kChunks>();
+    for (int base = 0; base < n; base += 8 * kRPL) {
+      uint32_t id[kRPL];
+      bool act[kRPL];
+      const float *row[kRPL];
+      float4 y[kRPL][kChunks];
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) {
+        const int idx = base + g + 8 * r;
+        act[r] = idx < n;
+        id[r] = act[r] ? ids[idx] : 0u;
+        row[r] = p.base + static_cast<uint64_t>(id[r]) * p.stride;
+      }
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) {
+        const float4 *rp = reinterpret_cast<const float4 *>(row[r]) + m;
+        if (act[r]) {
+#pragma unroll
+          for (int t = 0; t < kChunks; ++t) y[r][t] = rp[8 * t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < kChunks; ++t) y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      float a[kRPL][4];
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
+      const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+#pragma unroll
+      for (int t = 0; t < kChunks; ++t) {
+        const float4 x = qp[8 * t];
+#pragma unroll
+        for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
+      }
+#pragma unroll
+      for (int r = 0; r < kRPL; ++r) {
+        if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
+          for (int b = 0; b < nb8; ++b) {
+            const int e = 32 * T + 8 * b + 4 * m;
+            if (act[r]) {
+              accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
+                              *reinterpret_cast<const float4 *>(row[r] + e), a[r][0], a[r][1], a[r][2], a[r][3]);
+            }
+          }
+        }
+        const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
+        if (act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row[r], tail_begin, res, id[r]);
+      }
+    }
+  } else {
+    for (int base = 0; base < n; base += 8) {
+      const int r = base + g;
+      const bool act = r < n;
+      const uint32_t id = act ? ids[r] : 0u;
+      const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      if (act) {
+        const float4 *rp = reinterpret_cast<const float4 *>(row) + m;
+        const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+#pragma unroll 8
+        for (int t = 0; t < T; ++t) accumulate<kIP>(qp[8 * t], rp[8 * t], a0, a1, a2, a3);
+        if (m < 2) {
+          for (int b = 0; b < nb8; ++b) {
+            const int e = 32 * T + 8 * b + 4 * m;
+            accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
+                            *reinterpret_cast<const float4 *>(row + e), a0, a1, a2, a3);
+          }
+        }
+      }
+      const float res = finish_row<kIP>(a0, a1, a2, a3);
+      if (act && m == 0) out[r] = finish_tail<kIP>(p, q, row, tail_begin, res, id);
+    }
+  }
+  wave_sync();
+}
+
+// --------------------------------------------------------------------------------------------
+// SQ8 distances (SQ8Space::QueryComputer over l2_sqr_sq8 / ip_sqr_sq8).  The reference picks the
+// AVX-512 kernel when the host has AVX-512F, else AVX2 (distance_l2.ipp:694-708,
+// distance_ip.ipp:703-716).  Both are "P partial sums, element P*t+j -> acc[j]":
+//   AVX-512 (:334-408 / :292-366): P = 32 (sum0 = acc[0..15], sum1 = acc[16..31]); a trailing
+//     16-block feeds acc[0..15]; combine a = sum0+sum1, then GCC 11 _mm512_reduce_add_ps:
+//     T3[j] = a[8+j]+a[j], T6[j] = T3[4+j]+T3[j], r = (T6[0]+T6[2]) + (T6[1]+T6[3]).
+//   AVX2 (:244-329 / :198-287): P = 16 (sum0 = acc[0..7], sum1 = acc[8..15]); a trailing 8-block
+//     feeds acc[0..7]; combine v = sum0+sum1, s[j] = v[j]+v[j+4], r = (s0+s1)+(s2+s3).
+// Per element: scale = (max-min)*(1/255); L2: d = (x-y)*scale, acc = fma(d,d,acc);
+// IP: xv = fma(x,scale,min), yv = fma(y,scale,min), acc = fma(xv,yv,acc).  Scalar tail the same.
+// Two lanes per row (lane h owns acc[h*P/2 ...]): one pass covers 32 rows.  LDS holds, per
+// dimension, the query term (x for L2, xv for IP), scale and min.
+// --------------------------------------------------------------------------------------------
+template <bool kIP>
+__device__ __forceinline__ float sq8_term(float xq, float scale, float mn, float yf, float acc) {
+  if (kIP) return fmaf(xq, fmaf(yf, scale, mn), acc);
+  const float d = (xq - yf) * scale;
+  return fmaf(d, d, acc);
+}
+
+template <bool kIP, int kOrder, int kFull>
+__device__ __forceinline__ void sq8_distances(const SearchParams &p, const float *xq,
+                                              const float *sc, const float *mnv,
+                                              const uint32_t *ids, int n, float *out) {
+  constexpr int P = kOrder == 2 ? 32 : 16;
+  constexpr int H = P / 2;
+  constexpr int W = H / 4;  // 32-bit words per lane per chunk
+  const int lane = lane_id();
+  const int g = lane >> 1, h = lane & 1;
+  const int T = kFull > 0 ? kFull : static_cast<int>(p.dim) / P;
+  const int rem = static_cast<int>(p.dim) - P * T;
+  const bool half = rem >= H;
+  const int tail_begin = P * T + (half ? H : 0);
+  for (int base = 0; base < n; base += 32) {
+    const int r = base + g;
+    const bool act = r < n;
+    const uint32_t id = act ? ids[r] : 0u;
+    const uint8_t *row = p.codes + static_cast<uint64_t>(id) * p.code_stride;
+    float acc[H];
+#pragma unroll
+    for (int l = 0; l < H; ++l) acc[l] = 0.f;
+    auto chunk = [&](int t, const uint32_t *w, int hh) {
+#pragma unroll
+      for (int l = 0; l < H; ++l) {
+        const int e = P * t + H * hh + l;
+        const float yf = static_cast<float>((w[l >> 2] >> (8 * (l & 3))) & 0xffu);
+        acc[l] = sq8_term<kIP>(xq[e], sc[e], mnv[e], yf, acc[l]);
+      }
+    };
+    if (act) {
+      if constexpr (kFull > 0) {
+        uint32_t w[kFull][W];
+#pragma unroll
+        for (int t = 0; t < kFull; ++t) {
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * t + H * h);
+#pragma unroll
+          for (int q = 0; q < W; ++q) w[t][q] = src[q];
+        }
+#pragma unroll
+        for (int t = 0; t < kFull; ++t) chunk(t, w[t], h);
+      } else {
+        for (int t = 0; t < T; ++t) {
+          uint32_t w[W];
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * t + H * h);
+#pragma unroll
+          for (int q = 0; q < W; ++q) w[q] = src[q];
+          chunk(t, w, h);
+        }
+      }
+      if (half && h == 0) {  // trailing half block -> sum0
+        uint32_t w[W];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * T);
+#pragma unroll
+        for (int q = 0; q < W; ++q) w[q] = src[q];
+        chunk(T, w, 0);
+      }
+    }
+    float res;
+#pragma unroll
+    for (int l = 0; l < H; ++l) acc[l] += __shfl_xor(acc[l], 1);  // sum0 + sum1
+    if constexpr (kOrder == 2) {
+      float t3[8], t6[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t3[j] = acc[8 + j] + acc[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t6[j] = t3[4 + j] + t3[j];
+      res = (t6[0] + t6[2]) + (t6[1] + t6[3]);
+    } else {
+      float s4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s4[j] = acc[j] + acc[j + 4];
+      res = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    }
+    if (act && h == 0) {
+      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
+        res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(row[e]), res);
+      out[r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
+    }
+  }
+  wave_sync();
+}
+
+template <bool kIP, int kChunks, int kSpace>
+__device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
+                                                const uint32_t *ids, int n, float *out) {
+  if constexpr (kSpace == 0) {
+    row_distances<kIP, kChunks>(p, L.q, ids, n, out);
+  } else {
+    sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks>(p, L.q, L.sq_scale, L.sq_min, ids, n, out);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Visited set: exact (DynamicBitset semantics, query_utils.hpp:69-115).  First level: an LDS
+// open-addressing table with linear probing.  Two layouts:
+//   wide    -- 32-bit slots holding the id (kEmpty = free);
+//   compact -- 16-bit slots.  h = (v * C) mod 2^L is a bijection on [0, 2^L) (C odd,
+//              L = vis_lbits >= log2 n); the home slot is the top log2h bits of h and the slot
+//              stores 1 + (probe distance << rbits | low rbits bits of h), so (slot, entry)
+//              identifies v exactly in half the bytes: twice the entries per LDS byte.
+// When the table passes its load limit (or a compact probe would exceed the encodable distance)
+// the query spills: a per-slot global N-bit bitset becomes the second level (atomicOr).
+// --------------------------------------------------------------------------------------------
+struct Visited {
+  uint32_t *tab;
+  uint32_t log2h;
+  uint32_t count;        // wave-uniform number of entries in the LDS table
+  uint32_t limit;        // switch to the global bitset above this many entries
+  bool spilled;          // wave-uniform
+  uint32_t *bits;        // per-slot global bitset (valid when spilled)
+  uint32_t rbits;        // compact: remainder bits; kVisWide: 32-bit slots
+  uint32_t lmask;        // compact: 2^L - 1
+  uint32_t lshift;       // compact, L < log2h: home = h << lshift
+  uint32_t max_disp;     // compact: largest encodable probe distance
+};
+
+__device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t *tab, uint32_t *bits) {
+  Visited vs;
+  vs.tab = tab;
+  vs.log2h = p.hash_log2;
+  vs.count = 0u;
+  vs.spilled = false;
+  vs.bits = bits;
+  vs.rbits = p.vis_rbits;
+  const uint32_t hsize = 1u << p.hash_log2;
+  if (p.vis_rbits == kVisWide) {
+    vs.limit = hsize / 2;
+    vs.lmask = vs.lshift = vs.max_disp = 0u;
+  } else {
+    vs.limit = hsize - hsize / 4 - hsize / 16;  // load factor 0.69
+    vs.lmask = p.vis_lbits >= 32 ? 0xffffffffu : (1u << p.vis_lbits) - 1u;
+    vs.lshift = p.vis_lbits < p.hash_log2 ? p.hash_log2 - p.vis_lbits : 0u;
+    vs.max_disp = p.vis_max_disp;
+  }
+  return vs;
+}
+
+__device__ __forceinline__ void compact_key(const Visited &vs, uint32_t v, uint32_t &home, uint32_t &rem) {
+  const uint32_t h = (v * 0x9E3779B1u) & vs.lmask;
+  if (vs.rbits) {
+    home = h >> vs.rbits;
+    rem = h & ((1u << vs.rbits) - 1u);
+  } else {
+    home = h << vs.lshift;
+    rem = 0u;
+  }
+}
+
+__device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
+  const uint32_t mask = (1u << vs.log2h) - 1u;
+  if (vs.rbits == kVisWide) {
+    uint32_t h = hash_slot(v, vs.log2h);
+    for (;;) {
+      const uint32_t e = vs.tab[h];
+      if (e == v) return true;
+      if (e == kEmpty) return false;
+      h = (h + 1) & mask;
+    }
+  }
+  uint32_t home, rem;
+  compact_key(vs, v, home, rem);
+  const uint16_t *t16 = reinterpret_cast<const uint16_t *>(vs.tab);
+  for (uint32_t i = 0;; ++i) {
+    const uint32_t e = t16[(home + i) & mask];
+    if (e == 0u) return false;
+    if (e == 1u + ((i << vs.rbits) | rem)) return true;
+    if (i == vs.max_disp) return false;  // inserts never go further
+  }
+}
+
+// Insert into the LDS table.  Returns 1 = inserted (fresh), 0 = already present, 2 = compact probe
+// ran past max_disp (not present, not inserted: the caller spills).
+__device__ __forceinline__ int table_insert(const Visited &vs, uint32_t v) {
+  const uint32_t mask = (1u << vs.log2h) - 1u;
+  if (vs.rbits == kVisWide) {
+    uint32_t h = hash_slot(v, vs.log2h);
+    for (;;) {
+      const uint32_t old = atomicCAS(&vs.tab[h], kEmpty, v);
+      if (old == kEmpty) return 1;
+      if (old == v) return 0;
+      h = (h + 1) & mask;
+    }
+  }
+  uint32_t home, rem;
+  compact_key(vs, v, home, rem);
+  for (uint32_t i = 0; i <= vs.max_disp; ++i) {
+    const uint32_t slot = (home + i) & mask;
+    uint32_t *w = &vs.tab[slot >> 1];
+    const uint32_t sh = (slot & 1u) * 16u;
+    const uint32_t mine = 1u + ((i << vs.rbits) | rem);
+    uint32_t cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+      const uint32_t e = (cur >> sh) & 0xffffu;
+      if (e == mine) return 0;
+      if (e != 0u) break;  // occupied by another key: next slot
+      const uint32_t old = atomicCAS(w, cur, cur | (mine << sh));
+      if (old == cur) return 1;
+      cur = old;  // the other half of the word (or this slot) changed: re-examine
+    }
+  }
+  return 2;
+}
+
+__device__ void spill_begin(Visited &vs, uint64_t n_words) {
+  // zero this slot's global bitset once, then keep the LDS table as a read-only first level.
+  const int lane = lane_id();
+  for (uint64_t w = lane; w < n_words; w += 64) vs.bits[w] = 0u;
+  __threadfence_block();
+  wave_sync();
+  vs.spilled = true;
+}
+
+__device__ __forceinline__ bool global_visit(const Visited &vs, uint32_t v) {
+  const uint32_t bit = 1u << (v & 31);
+  const uint32_t old = atomicOr(&vs.bits[v >> 5], bit);
+  return (old & bit) == 0u;
+}
+
+// All lanes with `act` insert their v; duplicates among lanes must have been removed.
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, uint64_t n_words) {
+  bool fresh = false;
+  if (!vs.spilled) {
+    int r = 0;
+    if (act) r = table_insert(vs, v);
+    fresh = r == 1;
+    vs.count += __popcll(ballot(fresh));
+    if (ballot(r == 2)) {  // a compact probe ran out of encodable distance: spill now
+      spill_begin(vs, n_words);
+      if (r == 2) fresh = global_visit(vs, v);
+    }
+  } else if (act) {
+    if (!table_lookup(vs, v)) fresh = global_visit(vs, v);
+  }
+  return fresh;
+}
+
+// --------------------------------------------------------------------------------------------
+// Pool (LinearPool).  size/cur are wave-uniform.  Checked flag lives in bit 31 of the id.
+// --------------------------------------------------------------------------------------------
+struct PoolState {
+  uint32_t size;
+  uint32_t cur;
+  uint32_t ef;
+};
+
+// number of pool entries with dist <= d (find_bsearch, strict '>' keeps equal ones first)
+__device__ __forceinline__ uint32_t pool_upper_bound(const float *pd, uint32_t size, float d) {
+  uint32_t lo = 0, hi = size;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pd[mid] > d) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+// number of sorted batch distances strictly below d
+__device__ __forceinline__ uint32_t batch_lower_bound(const float *sd, uint32_t n, float d) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sd[mid] < d) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Merge candidates held by lanes 0..nb-1 (arrival order = lane order, nb <= 64) into the pool.
+// Equivalent to calling LinearPool::insert(id_i, d_i) for i = 0..nb-1 in order.
+__device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d) {
+  const int lane = lane_id();
+  const bool full = ps.size == ps.ef;
+  const float last = full ? L.pd[ps.size - 1] : 0.f;
+  const bool acc = has && !(full && d >= last);
+  const uint64_t amask = ballot(acc);
+  const uint32_t n_acc = __popcll(amask);
+  if (n_acc == 0) return;
+  // stable rank of this candidate among accepted ones, ordered by (dist, arrival)
+  uint32_t rank = 0;
+  uint64_t rest = amask;
+  while (rest) {
+    const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
+    rest &= rest - 1;
+    const float dj = __shfl(d, j);
+    rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
+  }
+  if (acc) L.sd[rank] = d;
+  uint32_t pos = 0;
+  if (acc) pos = pool_upper_bound(L.pd, ps.size, d) + rank;
+  // first insertion position = position of the rank-0 element
+  const uint32_t first_pos = __shfl(pos, __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1);
+  wave_sync();
+  // shift pool entries [first_pos, size) up by #accepted strictly smaller, top chunk first.
+  for (int hi = static_cast<int>(ps.size); hi > static_cast<int>(first_pos); hi -= 64) {
+    const int j = hi - 64 + lane;
+    const bool mv = j >= static_cast<int>(first_pos);
+    float pdj = 0.f;
+    uint32_t pij = 0;
+    uint32_t dest = 0;
+    if (mv) {
+      pdj = L.pd[j];
+      pij = L.pi[j];
+      dest = static_cast<uint32_t>(j) + batch_lower_bound(L.sd, n_acc, pdj);
+    }
+    wave_sync();
+    if (mv && dest < ps.ef) {
+      L.pd[dest] = pdj;
+      L.pi[dest] = pij;
+    }
+    wave_sync();
+  }
+  if (acc && pos < ps.ef) {
+    L.pd[pos] = d;
+    L.pi[pos] = id;
+  }
+  wave_sync();
+  ps.size = min(ps.size + n_acc, ps.ef);
+  if (first_pos < ps.cur) ps.cur = first_pos;
+}
+
+// LinearPool::pop: mark cur checked, advance to the next unchecked entry.
+__device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L) {
+  const int lane = lane_id();
+  const uint32_t raw = L.pi[ps.cur];
+  wave_sync();
+  if (lane == 0) L.pi[ps.cur] = raw | kChecked;
+  uint32_t next = ps.size;
+  for (uint32_t b = ps.cur + 1; b < ps.size; b += 64) {
+    const uint32_t j = b + lane;
+    const bool un = j < ps.size && !(L.pi[j] & kChecked);
+    const uint64_t mk = ballot(un);
+    if (mk) {
+      next = b + __ffsll(static_cast<unsigned long long>(mk)) - 1;
+      break;
+    }
+  }
+  wave_sync();
+  ps.cur = next;
+  return raw & kIdMask;
+}
+
+}  // namespace
+}  // namespace alaya_amd

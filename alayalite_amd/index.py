@@ -29,7 +29,13 @@ class Index:
     def get_data_by_id(self, vector_id: int) -> VectorLike:
         return self.__index.get_data_by_id(vector_id)
 
-    def fit(self, vectors: VectorLikeBatch, ef_construction: int = 100, num_threads: int = 1):
+    def fit(self, vectors: VectorLikeBatch, ef_construction: int = 100, num_threads: int = 1,
+            builder: str = "host"):
+        """index.py:75-99.  builder="host" builds the graph with the reference's HNSWBuilder restated
+        on the host (num_threads=1 gives the reference's graph exactly); builder="gpu" builds it on the
+        MI355X by batched insertion (alaya_index_build_graph) -- same algorithm, orders of magnitude
+        faster at 1M+ rows, graph not identical to the sequential one."""
+        _assert(builder in ("host", "gpu"), "builder must be 'host' or 'gpu'")
         if self.__is_initialized:
             raise RuntimeError("An index can be only fitted once")
         _assert(vectors.ndim == 2, "vectors must be a 2D array")
@@ -42,7 +48,7 @@ class Index:
         self.__dim = vectors.shape[1]
         self.__index = _PyIndexInterface(self.__params.to_cpp_params())
         self.__is_initialized = True
-        self.__index.fit(vectors, ef_construction, num_threads)
+        self.__index.fit(vectors, ef_construction, num_threads, builder)
 
     def insert(self, vectors: VectorLike, ef: int = 100):
         _assert(self.__index is not None, "Index is not init yet")

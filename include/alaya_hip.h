@@ -88,6 +88,23 @@ int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq,
 int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uint64_t nq,
                                     uint32_t k, uint32_t ef, uint32_t *d_ids, float *d_dists,
                                     uint32_t *d_counters, void *stream);
+/* ---- device graph construction (Index.fit on the MI355X) ------------------------------------
+ * Replaces HNSWBuilder::build_graph (include/index/graph/hnsw/hnsw_builder.hpp:98-194) over hnswlib
+ * add_point (include/index/graph/hnsw/hnswlib.hpp:652-751), from the index's own rows
+ * (alaya_index_set_base; COS rows already normalised).  M = R/2, M0 = R, ef = max(ef_construction,
+ * M), levels drawn exactly as the reference draws them from `seed` (100 in the reference).  Points
+ * are inserted in label order in batches of max(1, min(max_batch, inserted / batch_div)) (0 ->
+ * defaults 16 / 65536); within a batch every point runs searchBaseLayer + the neighbour heuristic
+ * on the device against the graph as it stood before the batch, then reverse edges are merged per
+ * destination (append, or prune with the heuristic).  `refine` extra level-0 passes per batch let
+ * the batch's points re-select among each other once they are linked in (1 recommended; with
+ * batch_div = max_batch = 1 and refine = 0 the insertion is sequential, as the reference's).  The result is installed as the index's
+ * search graph and a host copy is returned in *out (nullable).  stats (nullable, 8 x u64):
+ * batches, kernel launches, list prunes, appended edges, heuristic distances, device time (us),
+ * largest batch, max level. */
+int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_construction, uint64_t seed,
+                            uint32_t batch_div, uint32_t max_batch, uint32_t refine, alaya_graph **out,
+                            uint64_t *stats);
 /* ---- online updates (Index.insert / Index.remove) ------------------------------------------
  * Device-mirror primitives, for a host that keeps its own graph and update job (the reference's
  * GraphUpdateJob, include/executor/jobs/graph_update_job.hpp:49-137) and patches HBM after each
