@@ -45,7 +45,7 @@ struct BuildParams {
   uint64_t *edge_keys;       // nq x M: (neighbour << 32) | point, ~0 = unused (sorted in place)
   float *edge_d;             // nq x M: dist(point, neighbour)
   uint64_t n_edges;          // apply: edge slots (nq x M)
-  uint32_t *counters;        // optional: [0] prunes, [1] appends, [2] heuristic distances
+  unsigned long long *counters;  // optional: [0] prunes, [1] appends, [2] heuristic distances
 };
 
 size_t build_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact);

@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(64) build_select_kernel(BuildParams bp) {
     }
     wave_sync();
   }
-  if (bp.counters && lane == 0 && n_dist) atomicAdd(&bp.counters[2], n_dist);
+  if (bp.counters && lane == 0 && n_dist) atomicAdd(&bp.counters[2], static_cast<unsigned long long>(n_dist));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -371,9 +371,9 @@ __global__ void __launch_bounds__(64) build_apply_kernel(BuildParams bp) {
     }
   }
   if (bp.counters && lane == 0) {
-    if (n_prune) atomicAdd(&bp.counters[0], n_prune);
-    if (n_append) atomicAdd(&bp.counters[1], n_append);
-    if (n_dist) atomicAdd(&bp.counters[2], n_dist);
+    if (n_prune) atomicAdd(&bp.counters[0], static_cast<unsigned long long>(n_prune));
+    if (n_append) atomicAdd(&bp.counters[1], static_cast<unsigned long long>(n_append));
+    if (n_dist) atomicAdd(&bp.counters[2], static_cast<unsigned long long>(n_dist));
   }
 }
 

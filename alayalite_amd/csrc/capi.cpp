@@ -232,7 +232,6 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.code_stride = ix->code_stride;
     p.sq_min = ix->sq_min.as<float>();
     p.sq_max = ix->sq_max.as<float>();
-    p.stamps = nullptr;
   }
   p.hash_log2 = size_visited(ix, p, nq, ef);
   const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2, sq8, p.vis_rbits != alaya_amd::kVisWide);
@@ -885,8 +884,8 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
     size_t tmp_bytes = 0;
     hip_check(alaya_amd::sort_edges(nullptr, &tmp_bytes, nullptr, nullptr, nullptr, nullptr, n_edge_max, st), "sort size");
     sort_tmp.reserve(tmp_bytes);
-    cnt.reserve(8 * 4);
-    hip_check(hipMemsetAsync(cnt.ptr, 0, 8 * 4, st), "memset");
+    cnt.reserve(8 * 8);
+    hip_check(hipMemsetAsync(cnt.ptr, 0, 8 * 8, st), "memset");
     ix->work.reserve(4);
 
     alaya_amd::BuildParams bp{};
@@ -908,7 +907,7 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
     bp.cand_d = c_d.as<float>();
     bp.cand_n = c_n.as<uint32_t>();
     bp.M = M;
-    bp.counters = cnt.as<uint32_t>();
+    bp.counters = cnt.as<unsigned long long>();
     // visited-set sizing and the spill area for the largest batch (sized once: kernels in flight)
     {
       SearchParams probe = bp.s;
@@ -972,7 +971,7 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
     hip_check(hipMemcpyAsync(g.l0.data(), ix->l0.ptr, n * R * 4, hipMemcpyDeviceToHost, st), "D2H");
     if (n_upper)
       hip_check(hipMemcpyAsync(g.upper_edges.data(), ix->upper_edges.ptr, n_upper * 4, hipMemcpyDeviceToHost, st), "D2H");
-    uint32_t hc[8] = {0};
+    unsigned long long hc[8] = {0};
     hip_check(hipMemcpyAsync(hc, cnt.ptr, sizeof(hc), hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "device build");
     float ms = 0.f;
@@ -1039,7 +1038,7 @@ int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq,
 }
 
 int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
-                               uint32_t ef, uint32_t *ids, uint32_t *counters, uint64_t *stamps) {
+                               uint32_t ef, int space, uint32_t *ids, uint32_t *counters, uint64_t *stamps) {
   return guarded([&] {
     if (!ix || (nq && (!queries || !ids || !stamps))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
@@ -1053,7 +1052,7 @@ int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t n
     hip_check(hipMemsetAsync(st.ptr, 0, nq * 64, ix->stream), "memset");
     hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
     do_search(ix, ix->q_buf.as<float>(), nq, k, ef, ix->id_buf.as<uint32_t>(), nullptr,
-              ix->cnt_buf.as<uint32_t>(), ix->stream, st.as<uint64_t>());
+              ix->cnt_buf.as<uint32_t>(), ix->stream, st.as<uint64_t>(), space == 1);
     hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     if (counters)
       hip_check(hipMemcpyAsync(counters, ix->cnt_buf.ptr, nq * 16, hipMemcpyDeviceToHost, ix->stream), "D2H");

@@ -825,12 +825,12 @@ class DeviceIndex {
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
   void set_visited_mode(int m) { check(alaya_index_set_visited_mode(ix_, m)); }
   py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
-                           uint32_t ef) {
+                           uint32_t ef, int space) {
     const uint64_t nq = q.shape(0);
     py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
     py::array_t<uint32_t> c({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(4)});
     py::array_t<uint64_t> st({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(8)});
-    check(alaya_index_profile_search(ix_, q.data(), nq, k, ef, ids.mutable_data(), c.mutable_data(),
+    check(alaya_index_profile_search(ix_, q.data(), nq, k, ef, space, ids.mutable_data(), c.mutable_data(),
                                      st.mutable_data()));
     return py::make_tuple(ids, c, st);
   }
@@ -946,7 +946,8 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)
       .def("search_sq8", &DeviceIndex::search_sq8, py::arg("queries"), py::arg("k"), py::arg("ef"),
            py::arg("rerank") = 1, py::arg("rerank_queries") = py::none())
-      .def("profile_search", &DeviceIndex::profile_search)
+      .def("profile_search", &DeviceIndex::profile_search, py::arg("q"), py::arg("k"), py::arg("ef"),
+           py::arg("space") = 0)
       .def("device_bytes", &DeviceIndex::device_bytes);
   m.def("sq8_train", [](py::array_t<float, py::array::c_style | py::array::forcecast> data) {
     const uint32_t d = static_cast<uint32_t>(data.shape(1));

@@ -114,52 +114,54 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
   const int tail_begin = 32 * T + 8 * nb8;
   if constexpr (kChunks > 0) {
     constexpr int kRPL = rows_per_group<kChunks>();
-    for (int base = 0; base < n; base += 8 * kRPL) {
-      uint32_t id[kRPL];
-      bool act[kRPL];
-      const float *row[kRPL];
-      float4 y[kRPL][kChunks];
+    {
+      for (int base = 0; base < n; base += 8 * kRPL) {
+        uint32_t id[kRPL];
+        bool act[kRPL];
+        const float *row[kRPL];
+        float4 y[kRPL][kChunks];
 #pragma unroll
-      for (int r = 0; r < kRPL; ++r) {
-        const int idx = base + g + 8 * r;
-        act[r] = idx < n;
-        id[r] = act[r] ? ids[idx] : 0u;
-        row[r] = p.base + static_cast<uint64_t>(id[r]) * p.stride;
-      }
-#pragma unroll
-      for (int r = 0; r < kRPL; ++r) {
-        const float4 *rp = reinterpret_cast<const float4 *>(row[r]) + m;
-        if (act[r]) {
-#pragma unroll
-          for (int t = 0; t < kChunks; ++t) y[r][t] = rp[8 * t];
-        } else {
-#pragma unroll
-          for (int t = 0; t < kChunks; ++t) y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int r = 0; r < kRPL; ++r) {
+          const int idx = base + g + 8 * r;
+          act[r] = idx < n;
+          id[r] = act[r] ? ids[idx] : 0u;
+          row[r] = p.base + static_cast<uint64_t>(id[r]) * p.stride;
         }
-      }
-      float a[kRPL][4];
 #pragma unroll
-      for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
-      const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+        for (int r = 0; r < kRPL; ++r) {
+          const float4 *rp = reinterpret_cast<const float4 *>(row[r]) + m;
+          if (act[r]) {
 #pragma unroll
-      for (int t = 0; t < kChunks; ++t) {
-        const float4 x = qp[8 * t];
+            for (int t = 0; t < kChunks; ++t) y[r][t] = rp[8 * t];
+          } else {
 #pragma unroll
-        for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
-      }
-#pragma unroll
-      for (int r = 0; r < kRPL; ++r) {
-        if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
-          for (int b = 0; b < nb8; ++b) {
-            const int e = 32 * T + 8 * b + 4 * m;
-            if (act[r]) {
-              accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
-                              *reinterpret_cast<const float4 *>(row[r] + e), a[r][0], a[r][1], a[r][2], a[r][3]);
-            }
+            for (int t = 0; t < kChunks; ++t) y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
-        const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
-        if (act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row[r], tail_begin, res, id[r]);
+        float a[kRPL][4];
+#pragma unroll
+        for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
+        const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+#pragma unroll
+        for (int t = 0; t < kChunks; ++t) {
+          const float4 x = qp[8 * t];
+#pragma unroll
+          for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
+        }
+#pragma unroll
+        for (int r = 0; r < kRPL; ++r) {
+          if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
+            for (int b = 0; b < nb8; ++b) {
+              const int e = 32 * T + 8 * b + 4 * m;
+              if (act[r]) {
+                accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
+                                *reinterpret_cast<const float4 *>(row[r] + e), a[r][0], a[r][1], a[r][2], a[r][3]);
+              }
+            }
+          }
+          const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
+          if (act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row[r], tail_begin, res, id[r]);
+        }
       }
     }
   } else {
@@ -200,8 +202,11 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
 //     feeds acc[0..7]; combine v = sum0+sum1, s[j] = v[j]+v[j+4], r = (s0+s1)+(s2+s3).
 // Per element: scale = (max-min)*(1/255); L2: d = (x-y)*scale, acc = fma(d,d,acc);
 // IP: xv = fma(x,scale,min), yv = fma(y,scale,min), acc = fma(xv,yv,acc).  Scalar tail the same.
-// Two lanes per row (lane h owns acc[h*P/2 ...]): one pass covers 32 rows.  LDS holds, per
-// dimension, the query term (x for L2, xv for IP), scale and min.
+// P/4 lanes per row (8 for AVX-512, 4 for AVX2): lane m owns acc[4m..4m+3], i.e. one code dword
+// per P-byte chunk, so every partial sum stays one sequential chain as on the host.  The combine
+// is a shuffle tree inside the row's lanes (xor 4 / 2 / 1).  Each lane group takes kRPL rows per
+// pass; row slices past n are skipped wave-uniformly.  LDS holds, per dimension, the query term
+// (x for L2, xv for IP), scale and min, read as float4 for the lane's 4 dimensions.
 // --------------------------------------------------------------------------------------------
 template <bool kIP>
 __device__ __forceinline__ float sq8_term(float xq, float scale, float mn, float yf, float acc) {
@@ -210,83 +215,96 @@ __device__ __forceinline__ float sq8_term(float xq, float scale, float mn, float
   return fmaf(d, d, acc);
 }
 
+template <bool kIP>
+__device__ __forceinline__ void sq8_chunk(const float *xq, const float *sc, const float *mnv, int e,
+                                          uint32_t w, float *acc) {
+  const float4 x = *reinterpret_cast<const float4 *>(xq + e);
+  const float4 s = *reinterpret_cast<const float4 *>(sc + e);
+  float4 mn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (kIP) mn = *reinterpret_cast<const float4 *>(mnv + e);
+  acc[0] = sq8_term<kIP>(x.x, s.x, mn.x, static_cast<float>(w & 0xffu), acc[0]);
+  acc[1] = sq8_term<kIP>(x.y, s.y, mn.y, static_cast<float>((w >> 8) & 0xffu), acc[1]);
+  acc[2] = sq8_term<kIP>(x.z, s.z, mn.z, static_cast<float>((w >> 16) & 0xffu), acc[2]);
+  acc[3] = sq8_term<kIP>(x.w, s.w, mn.w, static_cast<float>(w >> 24), acc[3]);
+}
+
+// rows per lane group per pass: <= 48 code dwords in flight per lane (the per-chunk float4 LDS
+// reads are hoisted too; more rows spill at d = 768)
+template <int kOrder, int kFull>
+constexpr int sq8_rows_per_group() {
+  return kFull <= 0 ? 1 : (48 / kFull >= 4 ? 4 : (48 / kFull < 1 ? 1 : 48 / kFull));
+}
+
 template <bool kIP, int kOrder, int kFull>
 __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float *xq,
                                               const float *sc, const float *mnv,
                                               const uint32_t *ids, int n, float *out) {
   constexpr int P = kOrder == 2 ? 32 : 16;
-  constexpr int H = P / 2;
-  constexpr int W = H / 4;  // 32-bit words per lane per chunk
+  constexpr int LPR = P / 4;    // lanes per row
+  constexpr int G = 64 / LPR;   // row groups per wave
+  constexpr int kRPL = sq8_rows_per_group<kOrder, kFull>();
   const int lane = lane_id();
-  const int g = lane >> 1, h = lane & 1;
+  const int g = lane / LPR, m = lane % LPR;
   const int T = kFull > 0 ? kFull : static_cast<int>(p.dim) / P;
   const int rem = static_cast<int>(p.dim) - P * T;
-  const bool half = rem >= H;
-  const int tail_begin = P * T + (half ? H : 0);
-  for (int base = 0; base < n; base += 32) {
-    const int r = base + g;
-    const bool act = r < n;
-    const uint32_t id = act ? ids[r] : 0u;
-    const uint8_t *row = p.codes + static_cast<uint64_t>(id) * p.code_stride;
-    float acc[H];
+  const bool half = rem >= P / 2;
+  const int tail_begin = P * T + (half ? P / 2 : 0);
+  for (int base = 0; base < n; base += G * kRPL) {
+    uint32_t id[kRPL];
+    bool act[kRPL];
+    const uint8_t *row[kRPL];
+    float acc[kRPL][4];
 #pragma unroll
-    for (int l = 0; l < H; ++l) acc[l] = 0.f;
-    auto chunk = [&](int t, const uint32_t *w, int hh) {
-#pragma unroll
-      for (int l = 0; l < H; ++l) {
-        const int e = P * t + H * hh + l;
-        const float yf = static_cast<float>((w[l >> 2] >> (8 * (l & 3))) & 0xffu);
-        acc[l] = sq8_term<kIP>(xq[e], sc[e], mnv[e], yf, acc[l]);
-      }
-    };
-    if (act) {
-      if constexpr (kFull > 0) {
-        uint32_t w[kFull][W];
-#pragma unroll
-        for (int t = 0; t < kFull; ++t) {
-          const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * t + H * h);
-#pragma unroll
-          for (int q = 0; q < W; ++q) w[t][q] = src[q];
-        }
-#pragma unroll
-        for (int t = 0; t < kFull; ++t) chunk(t, w[t], h);
-      } else {
-        for (int t = 0; t < T; ++t) {
-          uint32_t w[W];
-          const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * t + H * h);
-#pragma unroll
-          for (int q = 0; q < W; ++q) w[q] = src[q];
-          chunk(t, w, h);
-        }
-      }
-      if (half && h == 0) {  // trailing half block -> sum0
-        uint32_t w[W];
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(row + P * T);
-#pragma unroll
-        for (int q = 0; q < W; ++q) w[q] = src[q];
-        chunk(T, w, 0);
-      }
+    for (int r = 0; r < kRPL; ++r) {
+      const int idx = base + g + G * r;
+      act[r] = idx < n;
+      id[r] = act[r] ? ids[idx] : 0u;
+      row[r] = p.codes + static_cast<uint64_t>(id[r]) * p.code_stride;
+      acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0.f;
     }
-    float res;
+    if constexpr (kFull > 0) {
+      uint32_t w[kRPL][kFull];
 #pragma unroll
-    for (int l = 0; l < H; ++l) acc[l] += __shfl_xor(acc[l], 1);  // sum0 + sum1
-    if constexpr (kOrder == 2) {
-      float t3[8], t6[4];
+      for (int r = 0; r < kRPL; ++r) {
+        if (base + G * r >= n) break;  // wave-uniform
 #pragma unroll
-      for (int j = 0; j < 8; ++j) t3[j] = acc[8 + j] + acc[j];
+        for (int t = 0; t < kFull; ++t)
+          w[r][t] = act[r] ? *reinterpret_cast<const uint32_t *>(row[r] + P * t + 4 * m) : 0u;
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) t6[j] = t3[4 + j] + t3[j];
-      res = (t6[0] + t6[2]) + (t6[1] + t6[3]);
+      for (int r = 0; r < kRPL; ++r) {
+        if (base + G * r >= n) break;
+#pragma unroll
+        for (int t = 0; t < kFull; ++t) sq8_chunk<kIP>(xq, sc, mnv, P * t + 4 * m, w[r][t], acc[r]);
+      }
     } else {
-      float s4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s4[j] = acc[j] + acc[j + 4];
-      res = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      if (act[0]) {
+        for (int t = 0; t < T; ++t)
+          sq8_chunk<kIP>(xq, sc, mnv, P * t + 4 * m, *reinterpret_cast<const uint32_t *>(row[0] + P * t + 4 * m),
+                         acc[0]);
+      }
     }
-    if (act && h == 0) {
-      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
-        res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(row[e]), res);
-      out[r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
+#pragma unroll
+    for (int r = 0; r < kRPL; ++r) {
+      if (base + G * r >= n) break;
+      if (half && m < LPR / 2 && act[r])  // trailing half block -> acc[0 .. P/2)
+        sq8_chunk<kIP>(xq, sc, mnv, P * T + 4 * m, *reinterpret_cast<const uint32_t *>(row[r] + P * T + 4 * m),
+                       acc[r]);
+      float a0 = acc[r][0], a1 = acc[r][1], a2 = acc[r][2], a3 = acc[r][3];
+      if constexpr (kOrder == 2) {  // a = sum0 + sum1 (lanes m, m+4)
+        a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+      }
+      // AVX-512: T3 = a[8+j] + a[j]; AVX2: v = sum0 + sum1 (lanes m, m+2)
+      a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
+      // AVX-512: T6 = T3[4+j] + T3[j]; AVX2: s = v[j] + v[j+4] (lanes m, m+1)
+      a0 += __shfl_xor(a0, 1); a1 += __shfl_xor(a1, 1); a2 += __shfl_xor(a2, 1); a3 += __shfl_xor(a3, 1);
+      float res = kOrder == 2 ? (a0 + a2) + (a1 + a3) : (a0 + a1) + (a2 + a3);
+      if (act[r] && m == 0) {
+        const uint8_t *rw = row[r];
+        for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
+          res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(rw[e]), res);
+        out[base + g + G * r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
+      }
     }
   }
   wave_sync();

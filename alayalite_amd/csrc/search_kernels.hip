@@ -382,8 +382,9 @@ static const void *kernel_ptr() {
 }
 
 template <int kSpace>
-static const void *sq8_symbol(bool ip, uint32_t dim) {
+static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped) {
   const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
+  if (stamped && chunks == 24) return ip ? kernel_ptr<true, 24, true, kSpace>() : kernel_ptr<false, 24, true, kSpace>();
   if (chunks == 4) return ip ? kernel_ptr<true, 4, false, kSpace>() : kernel_ptr<false, 4, false, kSpace>();
   if (chunks == 24) return ip ? kernel_ptr<true, 24, false, kSpace>() : kernel_ptr<false, 24, false, kSpace>();
   if (chunks == 30) return ip ? kernel_ptr<true, 30, false, kSpace>() : kernel_ptr<false, 30, false, kSpace>();
@@ -391,8 +392,8 @@ static const void *sq8_symbol(bool ip, uint32_t dim) {
 }
 
 const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order) {
-  if (sq8_order == 2) return sq8_symbol<2>(ip, dim);
-  if (sq8_order == 1) return sq8_symbol<1>(ip, dim);
+  if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped);
+  if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped);
   const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
   if (stamped) {
     if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();

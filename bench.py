@@ -48,11 +48,12 @@ WORKLOADS = {
                   "metric_name": "QPS @ recall@10>=0.95, SIFT-128 L2, 1M base / 10k queries (config 3)",
                   "data": "synthetic (SIFT-shaped 1024-centre mixture, integer-valued, seeds 3/4; graph built by "
                           "the engine's HNSW builder R=32 efc=100)"},
-    "sq8-ip": {"gen": "text_like", "dim": 768, "nq": 1000, "metric": 1, "sq8": True,
-               "metric_name": "QPS @ recall@10>=0.95, 768-d IP, SQ8 search + f32 rerank, 1M base / 1k queries "
-                              "(config 5 shape at 1M)",
-               "data": "synthetic (text-embedding-shaped 4096-centre unit-sphere mixture, row-normalised, seeds 7/8; "
-                       "graph built on f32 rows with IP, R=32 efc=100; SQ8 codes of the same rows)"},
+    "sq8-ip": {"gen": "text_like", "dim": 768, "nq": 1000, "metric": 1, "sq8": True, "n": 10_000_000,
+               "metric_name": "QPS @ recall@10>=0.95, 768-d IP, SQ8 search + f32 rerank, 10M base / 1k queries "
+                              "(config 5)",
+               "data": "synthetic (text-embedding-shaped 4096-centre unit-sphere mixture, 12 latent dims, "
+                       "row-normalised, seeds 7/8; graph built on f32 rows with IP, R=32 efc=100; SQ8 codes of the "
+                       "same rows)"},
 }
 
 
@@ -66,7 +67,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=1_000_000)
+    p.add_argument("--n", type=int, default=0, help="0 = the workload's default (1M; 10M for sq8-ip)")
     p.add_argument("--nq", type=int, default=0, help="0 = the workload's default")
     p.add_argument("--dim", type=int, default=0, help="0 = the workload's default")
     p.add_argument("--efc", type=int, default=100)
@@ -74,6 +75,9 @@ def parse():
     p.add_argument("--target-recall", type=float, default=0.95)
     p.add_argument("--mode", choices=("shard", "replica"), default="shard")
     p.add_argument("--build-threads", type=int, default=0)
+    p.add_argument("--builder", choices=("auto", "host", "gpu"), default="auto",
+                   help="graph builder: host = HNSWBuilder restated on the host (cached), gpu = the "
+                        "device batched build (alaya_index_build_graph); auto = gpu from 2M rows up")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cache-dir", default=os.path.join(ROOT, "data_cache"))
@@ -88,7 +92,9 @@ def parse():
         w = WORKLOADS[a.workload]
         a.nq = a.nq or w["nq"]
         a.dim = a.dim or w["dim"]
+        a.n = a.n or w.get("n", 1_000_000)
     else:
+        a.n = a.n or 1_000_000
         a.nq = a.nq or 1000
         a.dim = a.dim or 128
     return a
@@ -126,15 +132,29 @@ def graph_for(native, base, efc, threads, cache_dir, tag, metric=0):
     return g, dt
 
 
-def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64, metric=0):
+def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64, metric=0,
+             chunk=1_000_000):
     """Exact top-k (L2, or IP = largest inner product): fp32 GEMM shortlist on the device, float64
-    re-rank on the host."""
-    bn = (base_dev * base_dev).sum(1) if metric == 0 else None
-    out = np.zeros((queries_host.shape[0], k), np.int64)
-    for s in range(0, queries_dev.shape[0], 256):
+    re-rank on the host.  The base is scanned in chunks of `chunk` rows: one GEMM operand above 2^31
+    elements (e.g. 10M x 768) is outside what the BLAS kernels index correctly."""
+    nq = queries_host.shape[0]
+    n = base_dev.shape[0]
+    out = np.zeros((nq, k), np.int64)
+    for s in range(0, nq, 256):
         q = queries_dev[s:s + 256]
-        d = bn[None, :] - 2.0 * (q @ base_dev.T) if metric == 0 else -(q @ base_dev.T)
-        idx = torch.topk(d, cand, dim=1, largest=False).indices.cpu().numpy()
+        best_d, best_i = None, None
+        for c0 in range(0, n, chunk):
+            b = base_dev[c0:c0 + chunk]
+            d = (b * b).sum(1)[None, :] - 2.0 * (q @ b.T) if metric == 0 else -(q @ b.T)
+            dv, di = torch.topk(d, min(cand, b.shape[0]), dim=1, largest=False)
+            di = di + c0
+            if best_d is None:
+                best_d, best_i = dv, di
+            else:
+                best_d, sel = torch.topk(torch.cat([best_d, dv], 1), min(cand, best_d.shape[1] + dv.shape[1]),
+                                         dim=1, largest=False)
+                best_i = torch.gather(torch.cat([best_i, di], 1), 1, sel)
+        idx = best_i.cpu().numpy()
         for j in range(idx.shape[0]):
             c = idx[j]
             x = base_host[c].astype(np.float64)
@@ -145,8 +165,10 @@ def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64
 
 
 def pmc_traffic(cfg):
-    """HBM traffic of the search kernel from the committed rocprofv3 PMC passes at this config
-    (tools/run_pmc.sh -> tools/pmc_summary.py -> profiles/r*/traffic.json); None if absent."""
+    """HBM traffic of the search kernel from the committed rocprofv3 PMC passes on this workload
+    (tools/run_pmc.sh -> tools/pmc_summary.py -> profiles/r*/traffic.json): the profile with the same
+    n / nq / dim / k and the nearest ef (the multi-threaded host build moves the operating point by a
+    few ef between runs); None if absent."""
     import glob
 
     best = None
@@ -155,9 +177,12 @@ def pmc_traffic(cfg):
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if all(t["config"].get(k) == v for k, v in cfg.items()):
-            best = (path, t)
-    return best
+        c = t["config"]
+        if all(c.get(k) == v for k, v in cfg.items() if k != "ef_search"):
+            gap = abs(c.get("ef_search", 0) - cfg["ef_search"])
+            if best is None or gap < best[2]:
+                best = (path, t, gap)
+    return None if best is None else best[:2]
 
 
 def choose_ef(probe):
@@ -288,10 +313,17 @@ def main():
         lo, hi = 0, args.n
         my_base = base
         tag = f"{w['gen']}_m{metric}" if w["gen"] != "gist_like" else "gist"
-    graph, build_s = graph_for(native, my_base, args.efc, threads, args.cache_dir, tag, metric)
+    builder = args.builder if args.builder != "auto" else ("gpu" if my_base.shape[0] >= 2_000_000 else "host")
     index = native.DeviceIndex(local)
     index.set_base(my_base, metric)
-    index.set_graph(graph)
+    if builder == "gpu":
+        t = time.time()
+        graph, bstats = index.build_graph(R, args.efc, 100, 0, 0, 1)
+        build_s = time.time() - t
+        log(f"device-built graph {my_base.shape} in {build_s:.1f}s ({bstats})")
+    else:
+        graph, build_s = graph_for(native, my_base, args.efc, threads, args.cache_dir, tag, metric)
+        index.set_graph(graph)
     sq8 = None
     if use_sq8:
         # SQ8Space::fit on the shard's rows (sq8_space.hpp:116-127); reduction order of the host's
@@ -407,7 +439,7 @@ def main():
         traffic_bytes = prof[1]["traffic_over_algorithmic"] * bytes_launch
         traffic = {"gbs": round(traffic_bytes / (kernel_ms * 1e-3) / 1e9, 1),
                    "bytes_per_launch": int(traffic_bytes),
-                   "source": os.path.relpath(prof[0], ROOT)}
+                   "source": f"{os.path.relpath(prof[0], ROOT)} (PMC at ef={prof[1]['config']['ef_search']})"}
     if args.dump_counters and rank == 0:
         np.save(args.dump_counters, cnt)
 
@@ -434,13 +466,13 @@ def main():
             "scaling": "weak" if (world > 1 and args.mode == "replica") else "strong",
             "vs_baseline": None,
             "dtype": "u8+f32" if use_sq8 else "f32",
-            "data": w["data"],
+            "data": w["data"] + ("; graph from the device HNSW build" if builder == "gpu" else ""),
             "config": {"workload": f"hnsw-{w['gen'].split('_')[0]}{args.dim}-{args.n // 1000}k-"
                                    f"{'ip-sq8' if use_sq8 else ('ip' if metric else 'l2')}-{nq}q",
                        "n_base": args.n, "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef,
                        "recall_at_10": r_at, "ef_sweep": sweep, "mode": args.mode if world > 1 else "single",
                        "parallelism": f"{args.mode}{world}" if world > 1 else "1gpu",
-                       "graph_build_s": round(build_s, 1)},
+                       "graph_build_s": round(build_s, 1), "graph_builder": builder},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["gbs"] if traffic else None,

@@ -136,9 +136,10 @@ int alaya_index_distances(alaya_index *ix, const float *queries, uint64_t nq, co
                           uint32_t n, float *out);
 /* Diagnostic build of the search kernel: also returns per-query s_memtime cycles per phase,
  * stamps[nq*8] = (init+descent, pop, adjacency+visited, distances, merge, expansions after the
- * visited table spilled, whole query, 0). Same ids as alaya_index_batch_search. */
+ * visited table spilled, whole query, adjacency-prefetch hits).  space 0 = f32 rows (same ids as
+ * alaya_index_batch_search), 1 = the SQ8 codes (no rerank; d = 768 is stamped, others run plain). */
 int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
-                               uint32_t ef, uint32_t *ids, uint32_t *counters, uint64_t *stamps);
+                               uint32_t ef, int space, uint32_t *ids, uint32_t *counters, uint64_t *stamps);
 /* ---- SQ8 search space (SQ8Space: include/space/sq8_space.hpp, quant/sq8.hpp) --------------------
  * Per-dimension min/max (SQ8Quantizer::fit, sq8.hpp:99-113) and codes (quantize, :118-130). */
 int alaya_sq8_train(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v);

@@ -249,3 +249,4 @@ def test_uint64_ids_and_int_dtype(native, c1):
     from alayalite_amd.utils import calc_gt, calc_recall
 
     assert calc_recall(ids, calc_gt(base, queries, 10)) >= 0.9
+

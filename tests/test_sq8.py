@@ -57,7 +57,7 @@ def _sq8_setup(native, orc, n, d, nq, metric, seed, order):
 @pytest.mark.gpu
 @pytest.mark.parametrize("order", [2, 1])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("d", [128, 768, 100, 40, 24, 7])
+@pytest.mark.parametrize("d", [128, 768, 960, 100, 48, 40, 24, 7])
 def test_sq8_search_and_rerank_bit_exact(native, orc, order, metric, d):
     base, q, g, codes, mn, mx, view = _sq8_setup(native, orc, 1500, d, 12, metric, d + order, order)
     dev = native.DeviceIndex(0)

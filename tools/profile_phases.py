@@ -25,24 +25,43 @@ def main():
     ap.add_argument("--ef", type=int, default=400)
     ap.add_argument("--hash-log2", type=int, default=0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--workload", choices=("gist", "sq8"), default="gist",
+                    help="sq8: config-5 data (768-d IP, device-built graph), stamped SQ8 traversal")
     args = ap.parse_args()
     import bench as b
     from alayalite_amd import _native
     from workloads.datasets import gist_like
 
     ext = _native._ext
-    base, queries = gist_like(args.n, args.nq, args.dim)
-    g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
-    dev = ext.DeviceIndex(0)
-    dev.set_base(base, 0)
-    dev.set_graph(g)
+    space = 0
+    if args.workload == "sq8":
+        from workloads.datasets import text_like
+
+        base, queries = text_like(args.n, args.nq, 768)
+        dev = ext.DeviceIndex(0)
+        dev.set_base(base, 1)
+        dev.build_graph(32, 100, 100, 0, 0, 1)
+        mn, mx = ext.sq8_train(base)
+        dev.set_sq8(ext.sq8_encode(base, mn, mx, b.host_threads()), mn, mx, ext.host_sq8_order())
+        space = 1
+    else:
+        base, queries = gist_like(args.n, args.nq, args.dim)
+        g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
+        dev = ext.DeviceIndex(0)
+        dev.set_base(base, 0)
+        dev.set_graph(g)
     if args.hash_log2:
         dev.set_hash_log2(args.hash_log2)
-    ids0, _, cnt0 = dev.search(queries, 10, args.ef)
+    def plain_search():
+        if space:
+            return dev.search_sq8(queries, 10, args.ef, 0, None)
+        return dev.search(queries, 10, args.ef)
+
+    ids0, _, cnt0 = plain_search()
     t = time.time()
-    ids0, _, cnt0 = dev.search(queries, 10, args.ef)
+    ids0, _, cnt0 = plain_search()
     plain = time.time() - t
-    ids, cnt, st = dev.profile_search(queries, 10, args.ef)
+    ids, cnt, st = dev.profile_search(queries, 10, args.ef, space)
     assert np.array_equal(ids, ids0)
     names = ["init+descent", "pop", "adj+visited", "distances", "merge", "spilled_expansions", "query_total"]
     mean = st.mean(0)

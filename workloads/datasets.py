@@ -6,8 +6,10 @@ a low intrinsic dimension; purely isotropic 960-d noise would make recall 0.95 u
 practical ef, so the low-rank part is what puts recall 0.95 inside the ef sweep.
 SIFT-shaped (C3): 1024 centres ~ U[0, 128)^128, point = round(centre + N(0, 12^2)) clipped [0, 255].
 Text-embedding-shaped (C5): 4096 centres on the unit sphere, point = centre + low-rank component
-(48 latent directions) + small isotropic noise, row-normalised (inner product = cosine).  As for
-GIST, the low-rank part keeps recall 0.95 inside the ef sweep.
+(12 latent directions, sigma 0.15) + isotropic noise (sigma 0.002), row-normalised (inner product =
+cosine).  Tuned at config 5's 10M rows (tools/sq8_recall.py, profiles/r01/c5_tuning.log): with 48
+latent directions and noise 0.01 recall saturates near 0.72 at 10M (0.86 at 1M); with these values
+the reference's SQ8 + rerank reaches 0.954 at ef 400.
 """
 
 from __future__ import annotations
@@ -58,10 +60,16 @@ def sift_like(n: int, nq: int, dim: int = 128, seed_base: int = 3, seed_query: i
 
 
 def text_like(n: int, nq: int, dim: int = 768, seed_base: int = 7, seed_query: int = 8,
-              n_centres: int = 4096, latent: int = 48, sigma_latent: float = 0.15,
-              sigma_noise: float = 0.01):
+              n_centres: int = 4096, latent: int = 12, sigma_latent: float = 0.15,
+              sigma_noise: float = 0.002, centres: str = "sphere"):
     rng = np.random.default_rng(777)
-    centres = rng.standard_normal((n_centres, dim)).astype(np.float32)
+    if centres == "orthant":  # GIST-style correlated centres U[0, 0.5]^dim, scaled to unit norm
+        centres = rng.uniform(0.0, 0.5, (n_centres, dim)).astype(np.float32)
+    elif centres == "subspace":  # topics on a 32-d subspace: neighbouring topics exist at any scale
+        g = (rng.standard_normal((32, dim)) / np.sqrt(dim)).astype(np.float32)
+        centres = rng.standard_normal((n_centres, 32)).astype(np.float32) @ g
+    else:
+        centres = rng.standard_normal((n_centres, dim)).astype(np.float32)
     centres /= np.linalg.norm(centres, axis=1, keepdims=True)
     basis = (rng.standard_normal((latent, dim)) / np.sqrt(dim)).astype(np.float32)
 
