@@ -495,7 +495,15 @@ __device__ __forceinline__ uint32_t batch_lower_bound(const float *sd, uint32_t 
 
 // Merge candidates held by lanes 0..nb-1 (arrival order = lane order, nb <= 64) into the pool.
 // Equivalent to calling LinearPool::insert(id_i, d_i) for i = 0..nb-1 in order.
-__device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d) {
+struct NoNext {
+  __device__ void operator()(uint32_t) const {}
+};
+
+// on_next(id) is called (wave-uniformly, before the shift) when the closest accepted candidate
+// lands at or before the first unchecked entry, i.e. when it is the next pop.
+template <typename OnNext = NoNext>
+__device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d,
+                           OnNext on_next = OnNext()) {
   const int lane = lane_id();
   const bool full = ps.size == ps.ef;
   const float last = full ? L.pd[ps.size - 1] : 0.f;
@@ -516,7 +524,9 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   uint32_t pos = 0;
   if (acc) pos = pool_upper_bound(L.pd, ps.size, d) + rank;
   // first insertion position = position of the rank-0 element
-  const uint32_t first_pos = __shfl(pos, __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1);
+  const int lane0 = __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1;
+  const uint32_t first_pos = __shfl(pos, lane0);
+  if (first_pos <= ps.cur) on_next(__shfl(id, lane0));
   wave_sync();
   // shift pool entries [first_pos, size) up by #accepted strictly smaller, top chunk first.
   for (int hi = static_cast<int>(ps.size); hi > static_cast<int>(first_pos); hi -= 64) {

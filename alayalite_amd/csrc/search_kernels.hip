@@ -211,8 +211,6 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       } else {
         v = lane < static_cast<int>(p.R) ? p.l0[static_cast<uint64_t>(u) * p.R + lane] : kEmpty;
       }
-      pred = ps.cur < ps.size ? (L.pi[ps.cur] & kIdMask) : kEmpty;
-      if (pred != kEmpty && lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(pred) * p.R + lane];
       const uint64_t endm = ballot(lane < static_cast<int>(p.R) && v == kEmpty);
       const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1 : static_cast<int>(p.R);
       bool act = lane < cnt;
@@ -226,6 +224,10 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       const bool fresh = visit(vs, v, act, bit_words);
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
+      // issue the prefetch only after v is consumed: a use of v behind a younger load would
+      // otherwise wait for that load too (vmcnt counts in issue order)
+      pred = ps.cur < ps.size ? (L.pi[ps.cur] & kIdMask) : kEmpty;
+      if (pred != kEmpty && lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(pred) * p.R + lane];
       stamp(2);
       if (nf == 0) continue;
       // compact fresh ids in adjacency order
@@ -239,7 +241,14 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       const uint32_t cid = has ? L.cid[lane] : 0u;
       const float cd = has ? L.cd[lane] : 0.f;
       wave_sync();
-      pool_merge(ps, L, has, cid, cd);
+      // the merge reports the next pop when it is a newcomer: load its adjacency row while the
+      // rest of the merge and the pop run (the prediction above is then stale)
+      pool_merge(ps, L, has, cid, cd, [&](uint32_t nx) {
+        if (nx != pred) {
+          pred = nx;
+          if (lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(nx) * p.R + lane];
+        }
+      });
       stamp(4);
     }
 

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--ef", type=int, default=400)
     ap.add_argument("--hash-log2", type=int, default=0)
     ap.add_argument("--out", default="")
-    ap.add_argument("--workload", choices=("gist", "sq8"), default="gist",
+    ap.add_argument("--workload", choices=("gist", "sq8", "sift"), default="gist",
                     help="sq8: config-5 data (768-d IP, device-built graph), stamped SQ8 traversal")
     args = ap.parse_args()
     import bench as b
@@ -44,6 +44,14 @@ def main():
         mn, mx = ext.sq8_train(base)
         dev.set_sq8(ext.sq8_encode(base, mn, mx, b.host_threads()), mn, mx, ext.host_sq8_order())
         space = 1
+    elif args.workload == "sift":
+        from workloads.datasets import sift_like
+
+        base, queries = sift_like(args.n, args.nq, 128)
+        g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "sift_like_m0")
+        dev = ext.DeviceIndex(0)
+        dev.set_base(base, 0)
+        dev.set_graph(g)
     else:
         base, queries = gist_like(args.n, args.nq, args.dim)
         g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
