@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
   for (;;) {
     uint32_t qi = 0;
     if (lane == 0) qi = atomicAdd(p.work_counter, 1u);
-    qi = __shfl(qi, 0);
+    qi = read_lane(qi, 0);
     if (qi >= p.nq) break;
     const uint32_t pt = bp.pts[qi];
     stage_row(p, pt, L.q);
@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
           for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
           const uint64_t at = ballot(has && dl == mn);
           if (at && mn < cur) {
-            u = __shfl(v, __ffsll(static_cast<unsigned long long>(at)) - 1);
+            u = read_lane(v, __ffsll(static_cast<unsigned long long>(at)) - 1);
             cur = mn;
             changed = true;
           }

@@ -29,6 +29,31 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// Lane exchanges without the LDS crossbar: xor 1 / xor 2 are quad-permute DPP moves (VALU), xor 4
+// is a bit-mode ds_swizzle (32-lane groups, no LDS access); a read of one uniform lane is a
+// v_readlane.  __shfl/__shfl_xor compile to ds_bpermute, an LDS-pipe round trip each.
+template <int kXor>
+__device__ __forceinline__ float lane_xor(float v) {
+  const int x = __builtin_bit_cast(int, v);
+  int r;
+  if constexpr (kXor == 1) {
+    r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (kXor == 2) {
+    r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else {
+    static_assert(kXor == 4 || kXor == 8 || kXor == 16, "lane_xor: 1, 2, 4, 8 or 16");
+    r = __builtin_amdgcn_ds_swizzle(x, (kXor << 10) | 0x1F);        // and 0x1f, xor kXor
+  }
+  return __builtin_bit_cast(float, r);
+}
+
+__device__ __forceinline__ float read_lane(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ uint32_t read_lane(uint32_t v, int l) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
+}
+
 __device__ __forceinline__ uint32_t hash_slot(uint32_t v, uint32_t log2h) {
   return (v * 0x9E3779B1u) >> (32 - log2h);
 }
@@ -72,11 +97,11 @@ __device__ __forceinline__ void accumulate(const float4 x, const float4 y, float
 template <bool kIP>
 __device__ __forceinline__ float finish_row(float a0, float a1, float a2, float a3) {
   // (acc0+acc1) + (acc2+acc3) per lane of the 8-wide vector: lanes m^2 then m^4.
-  a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
-  a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+  a0 += lane_xor<2>(a0); a1 += lane_xor<2>(a1); a2 += lane_xor<2>(a2); a3 += lane_xor<2>(a3);
+  a0 += lane_xor<4>(a0); a1 += lane_xor<4>(a1); a2 += lane_xor<4>(a2); a3 += lane_xor<4>(a3);
   // lane m==0 holds v[0..3], lane m==1 holds v[4..7]: s[j] = v[j] + v[j+4]; r = (s0+s1)+(s2+s3)
-  const float s0 = a0 + __shfl_xor(a0, 1), s1 = a1 + __shfl_xor(a1, 1);
-  const float s2 = a2 + __shfl_xor(a2, 1), s3 = a3 + __shfl_xor(a3, 1);
+  const float s0 = a0 + lane_xor<1>(a0), s1 = a1 + lane_xor<1>(a1);
+  const float s2 = a2 + lane_xor<1>(a2), s3 = a3 + lane_xor<1>(a3);
   return (s0 + s1) + (s2 + s3);
 }
 
@@ -292,12 +317,12 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
                        acc[r]);
       float a0 = acc[r][0], a1 = acc[r][1], a2 = acc[r][2], a3 = acc[r][3];
       if constexpr (kOrder == 2) {  // a = sum0 + sum1 (lanes m, m+4)
-        a0 += __shfl_xor(a0, 4); a1 += __shfl_xor(a1, 4); a2 += __shfl_xor(a2, 4); a3 += __shfl_xor(a3, 4);
+        a0 += lane_xor<4>(a0); a1 += lane_xor<4>(a1); a2 += lane_xor<4>(a2); a3 += lane_xor<4>(a3);
       }
       // AVX-512: T3 = a[8+j] + a[j]; AVX2: v = sum0 + sum1 (lanes m, m+2)
-      a0 += __shfl_xor(a0, 2); a1 += __shfl_xor(a1, 2); a2 += __shfl_xor(a2, 2); a3 += __shfl_xor(a3, 2);
+      a0 += lane_xor<2>(a0); a1 += lane_xor<2>(a1); a2 += lane_xor<2>(a2); a3 += lane_xor<2>(a3);
       // AVX-512: T6 = T3[4+j] + T3[j]; AVX2: s = v[j] + v[j+4] (lanes m, m+1)
-      a0 += __shfl_xor(a0, 1); a1 += __shfl_xor(a1, 1); a2 += __shfl_xor(a2, 1); a3 += __shfl_xor(a3, 1);
+      a0 += lane_xor<1>(a0); a1 += lane_xor<1>(a1); a2 += lane_xor<1>(a2); a3 += lane_xor<1>(a3);
       float res = kOrder == 2 ? (a0 + a2) + (a1 + a3) : (a0 + a1) + (a2 + a3);
       if (act[r] && m == 0) {
         const uint8_t *rw = row[r];
@@ -517,7 +542,7 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   while (rest) {
     const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
     rest &= rest - 1;
-    const float dj = __shfl(d, j);
+    const float dj = read_lane(d, j);
     rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
   }
   if (acc) L.sd[rank] = d;
@@ -525,8 +550,8 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   if (acc) pos = pool_upper_bound(L.pd, ps.size, d) + rank;
   // first insertion position = position of the rank-0 element
   const int lane0 = __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1;
-  const uint32_t first_pos = __shfl(pos, lane0);
-  if (first_pos <= ps.cur) on_next(__shfl(id, lane0));
+  const uint32_t first_pos = read_lane(pos, lane0);
+  if (first_pos <= ps.cur) on_next(read_lane(id, lane0));
   wave_sync();
   // shift pool entries [first_pos, size) up by #accepted strictly smaller, top chunk first.
   for (int hi = static_cast<int>(ps.size); hi > static_cast<int>(first_pos); hi -= 64) {

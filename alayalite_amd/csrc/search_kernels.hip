@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
   for (;;) {
     uint32_t qi = 0;
     if (lane == 0) qi = atomicAdd(p.work_counter, 1u);
-    qi = __shfl(qi, 0);
+    qi = read_lane(qi, 0);
     if (qi >= p.nq) break;
 
     uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
           const uint64_t at = ballot(has && dl == mn);
           if (at && mn < cur) {
             const int w = __ffsll(static_cast<unsigned long long>(at)) - 1;
-            u = __shfl(v, w);
+            u = read_lane(v, w);
             cur = mn;
             changed = true;
           }
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
         pool_merge(ps, L, has, v, d);
         // duplicates among eps are all inserted (no visited check in the reference loop)
         for (uint32_t j = 0; j < cnt; ++j) {
-          const uint32_t vj = __shfl(v, j);
+          const uint32_t vj = read_lane(v, j);
           if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
           visit(vs, vj, lane == 0, bit_words);
         }
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       bool act = lane < cnt;
       if (p.dedup_edges) {  // graphs with repeated ids in a row: keep the first occurrence only
         for (int j = 0; j < cnt; ++j) {
-          const uint32_t vj = __shfl(v, j);
+          const uint32_t vj = read_lane(v, j);
           if (j < lane && vj == v) act = false;
         }
       }
