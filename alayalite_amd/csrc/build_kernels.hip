@@ -59,11 +59,10 @@ __device__ __forceinline__ void stage_row(const SearchParams &p, uint32_t id, fl
 // the base point: keep a candidate unless an already kept one is closer to it than the base point
 // is (dist(kept, cand) < dist(base, cand)); stop at m kept.  Fewer than m candidates: keep all
 // (:296-298).  Returns the number kept; sel_i/sel_d (LDS, >= m entries) hold them in ascending
-// order.  q is an LDS row buffer, tmp an LDS scratch of >= m floats.
+// order.  tmp is an LDS scratch of >= m floats.
 template <bool kIP, int kChunks>
 __device__ uint32_t heuristic(const SearchParams &p, const uint32_t *ci, const float *cd, uint32_t C,
-                              uint32_t m, uint32_t *sel_i, float *sel_d, float *q, float *tmp,
-                              uint32_t *n_dist) {
+                              uint32_t m, uint32_t *sel_i, float *sel_d, float *tmp, uint32_t *n_dist) {
   const int lane = lane_id();
   if (C < m) {
     for (uint32_t j = lane; j < C; j += 64) {
@@ -79,8 +78,10 @@ __device__ uint32_t heuristic(const SearchParams &p, const uint32_t *ci, const f
     const float dc = cd[i];
     bool good = true;
     if (nsel > 0) {
-      stage_row(p, c, q);
-      row_distances<kIP, kChunks>(p, q, sel_i, static_cast<int>(nsel), tmp);
+      // the candidate's row is read straight from global memory (L2) by every row group, issued
+      // together with the kept rows' loads: one round trip per candidate instead of a staging
+      // copy into LDS first
+      row_distances<kIP, kChunks>(p, p.base + static_cast<uint64_t>(c) * p.stride, sel_i, static_cast<int>(nsel), tmp);
       good = ballot(lane < static_cast<int>(nsel) && tmp[lane] < dc) == 0;
       *n_dist += nsel;
       wave_sync();
@@ -232,8 +233,7 @@ template <bool kIP, int kChunks>
 __global__ void __launch_bounds__(64) build_select_kernel(BuildParams bp) {
   const SearchParams &p = bp.s;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float *q = reinterpret_cast<float *>(smem);
-  uint32_t *sel_i = reinterpret_cast<uint32_t *>(q + p.stride);
+  uint32_t *sel_i = reinterpret_cast<uint32_t *>(smem);
   float *sel_d = reinterpret_cast<float *>(sel_i + 64);
   float *tmp = sel_d + 64;
   const int lane = lane_id();
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(64) build_select_kernel(BuildParams bp) {
     const uint32_t pt = bp.pts[qi];
     const uint32_t C = bp.cand_n[qi];
     const uint32_t nsel = heuristic<kIP, kChunks>(p, bp.cand_ids + qi * p.ef, bp.cand_d + qi * p.ef, C, bp.M,
-                                                  sel_i, sel_d, q, tmp, &n_dist);
+                                                  sel_i, sel_d, tmp, &n_dist);
     // own list in the max-heap pop order: farthest first (hnswlib.hpp:527-551)
     uint32_t *row = adj_row_w(bp, pt, bp.level);
     for (uint32_t j = lane; j < W; j += 64) row[j] = j < nsel ? sel_i[nsel - 1 - j] : kEmpty;
@@ -265,8 +265,7 @@ __device__ void apply_segment(const BuildParams &bp, uint64_t s, unsigned char *
                               uint32_t *n_prune, uint32_t *n_append) {
   const SearchParams &p = bp.s;
   const int lane = lane_id();
-  float *q = reinterpret_cast<float *>(smem);
-  uint32_t *li = reinterpret_cast<uint32_t *>(q + p.stride);  // list in row order
+  uint32_t *li = reinterpret_cast<uint32_t *>(smem);  // list in row order
   float *ld = reinterpret_cast<float *>(li + kApplyCap);
   uint32_t *si = reinterpret_cast<uint32_t *>(ld + kApplyCap);  // sorted candidates
   float *sdd = reinterpret_cast<float *>(si + kApplyCap);
@@ -296,8 +295,7 @@ __device__ void apply_segment(const BuildParams &bp, uint64_t s, unsigned char *
   wave_sync();
   // distances of the existing list to v, needed once a prune is possible
   if (c + (e - s) > bp.Mmax) {
-    stage_row(p, v, q);
-    row_distances<kIP, kChunks>(p, q, li, static_cast<int>(c), ld);
+    row_distances<kIP, kChunks>(p, p.base + static_cast<uint64_t>(v) * p.stride, li, static_cast<int>(c), ld);
     *n_dist += c;
   }
   bool pruned = false;
@@ -333,7 +331,7 @@ __device__ void apply_segment(const BuildParams &bp, uint64_t s, unsigned char *
       sdd[r] = dj;
     }
     wave_sync();
-    const uint32_t nsel = heuristic<kIP, kChunks>(p, si, sdd, c, bp.Mmax, sel_i, sel_d, q, tmp, n_dist);
+    const uint32_t nsel = heuristic<kIP, kChunks>(p, si, sdd, c, bp.Mmax, sel_i, sel_d, tmp, n_dist);
     // pruned list in the max-heap pop order: farthest first (hnswlib.hpp:617-626)
     for (uint32_t j = lane; j < nsel; j += 64) {
       li[j] = sel_i[nsel - 1 - j];
@@ -410,8 +408,8 @@ const void *kernel_for(Which w, const SearchParams &p) {
   return sym<0>(w, p.ip);
 }
 
-size_t select_lds(uint32_t stride) { return static_cast<size_t>(stride) * 4 + 3 * 64 * 4; }
-size_t apply_lds(uint32_t stride) { return static_cast<size_t>(stride) * 4 + 4 * kApplyCap * 4 + 3 * 64 * 4; }
+size_t select_lds(uint32_t) { return 3 * 64 * 4; }
+size_t apply_lds(uint32_t) { return 4 * kApplyCap * 4 + 3 * 64 * 4; }
 
 hipError_t launch(Which w, const BuildParams &p, int grid, size_t lds, hipStream_t stream) {
   BuildParams arg = p;
