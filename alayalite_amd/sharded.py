@@ -32,12 +32,17 @@ def exchange_and_merge(local_ids, local_dists, offset: int, k: int, group=None):
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    device = local_ids.device
     gid = local_ids.to(torch.int64) + offset
+    ld = local_dists
+    if dist.get_backend(group) == "gloo" and device.type != "cpu":  # gloo gathers host tensors
+        gid, ld = gid.cpu(), ld.cpu()
     g_ids = [torch.empty_like(gid) for _ in range(world)]
-    g_d = [torch.empty_like(local_dists) for _ in range(world)]
+    g_d = [torch.empty_like(ld) for _ in range(world)]
     dist.all_gather(g_ids, gid, group=group)
-    dist.all_gather(g_d, local_dists, group=group)
-    return merge_topk(torch.cat(g_ids, 1), torch.cat(g_d, 1), k)
+    dist.all_gather(g_d, ld, group=group)
+    ids, d = merge_topk(torch.cat(g_ids, 1), torch.cat(g_d, 1), k)
+    return ids.to(device), d.to(device)
 
 
 def merge_reference(ids_per_shard, dists_per_shard, offsets, k):

@@ -67,7 +67,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=0, help="0 = the workload's default (1M; 10M for sq8-ip)")
+    p.add_argument("--n", "--n-base", dest="n", type=int, default=0,
+                   help="0 = the workload's default (1M; 10M for sq8-ip); --n-base under torchrun")
     p.add_argument("--nq", type=int, default=0, help="0 = the workload's default")
     p.add_argument("--dim", type=int, default=0, help="0 = the workload's default")
     p.add_argument("--efc", type=int, default=100)
@@ -288,8 +289,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ALAYA_BENCH_REHEARSE=1: every rank on cuda:0 with gloo -- rehearses the N-GPU code path
+    # (shards, exchange, merge, timing) on a one-GPU box; never used for reported numbers
+    rehearse = os.environ.get("ALAYA_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
