@@ -123,9 +123,11 @@ __device__ __forceinline__ float finish_tail(const SearchParams &p, const float 
 
 // rows per lane group per pass for a compile-time chunk count: keep the hoisted row chunks
 // within ~96 float4 (384 VGPRs) -- one wave per SIMD has the whole 512-entry register file.
+// Small rows (d <= 256): 2 rows per group = 16 rows per pass, which covers the ~10 fresh
+// neighbours of a typical expansion in one pass and leaves registers for more resident waves.
 template <int kChunks>
 constexpr int rows_per_group() {
-  return kChunks <= 0 ? 1 : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
+  return kChunks <= 0 ? 1 : kChunks <= 8 ? 2 : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
 }
 
 template <bool kIP, int kChunks>
