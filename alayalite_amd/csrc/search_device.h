@@ -130,6 +130,79 @@ constexpr int rows_per_group() {
   return kChunks <= 0 ? 1 : kChunks <= 8 ? 2 : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
 }
 
+// One pass of row loads in registers: lane group g (8 lanes) takes rows base + g + 8r, r < kR.
+template <int kChunks>
+struct RowPass {
+  static constexpr int kR = rows_per_group<kChunks>();
+  uint32_t id[kR];
+  bool act[kR];
+  float4 y[kR][kChunks];
+};
+
+// Issue every row chunk of the pass (all loads in flight before the first FMA).
+template <int kChunks>
+__device__ __forceinline__ void issue_rows(const SearchParams &p, const uint32_t *ids, int n, int base,
+                                           RowPass<kChunks> &P) {
+  constexpr int kRPL = RowPass<kChunks>::kR;
+  const int lane = lane_id();
+  const int g = lane >> 3, m = lane & 7;
+#pragma unroll
+  for (int r = 0; r < kRPL; ++r) {
+    const int idx = base + g + 8 * r;
+    P.act[r] = idx < n;
+    P.id[r] = P.act[r] ? ids[idx] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kRPL; ++r) {
+    const float4 *rp = reinterpret_cast<const float4 *>(p.base + static_cast<uint64_t>(P.id[r]) * p.stride) + m;
+    if (P.act[r]) {
+#pragma unroll
+      for (int t = 0; t < kChunks; ++t) P.y[r][t] = rp[8 * t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < kChunks; ++t) P.y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// Distances of an issued pass -> out[base + g + 8r].
+template <bool kIP, int kChunks>
+__device__ __forceinline__ void finish_rows(const SearchParams &p, const float *q, int base,
+                                            RowPass<kChunks> &P, float *out) {
+  constexpr int kRPL = RowPass<kChunks>::kR;
+  const int lane = lane_id();
+  const int g = lane >> 3, m = lane & 7;
+  constexpr int T = kChunks;
+  const int rem = static_cast<int>(p.dim) - 32 * T;
+  const int nb8 = rem >> 3;
+  const int tail_begin = 32 * T + 8 * nb8;
+  float a[kRPL][4];
+#pragma unroll
+  for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
+  const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
+#pragma unroll
+  for (int t = 0; t < kChunks; ++t) {
+    const float4 x = qp[8 * t];
+#pragma unroll
+    for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, P.y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
+  }
+#pragma unroll
+  for (int r = 0; r < kRPL; ++r) {
+    const float *row = p.base + static_cast<uint64_t>(P.id[r]) * p.stride;
+    if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
+      for (int b = 0; b < nb8; ++b) {
+        const int e = 32 * T + 8 * b + 4 * m;
+        if (P.act[r]) {
+          accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
+                          *reinterpret_cast<const float4 *>(row + e), a[r][0], a[r][1], a[r][2], a[r][3]);
+        }
+      }
+    }
+    const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
+    if (P.act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row, tail_begin, res, P.id[r]);
+  }
+}
+
 template <bool kIP, int kChunks>
 __device__ __forceinline__ void row_distances(const SearchParams &p, const float *q,
                                               const uint32_t *ids, int n, float *out) {
@@ -140,57 +213,13 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
   const int nb8 = rem >> 3;
   const int tail_begin = 32 * T + 8 * nb8;
   if constexpr (kChunks > 0) {
-    constexpr int kRPL = rows_per_group<kChunks>();
-    {
-      for (int base = 0; base < n; base += 8 * kRPL) {
-        uint32_t id[kRPL];
-        bool act[kRPL];
-        const float *row[kRPL];
-        float4 y[kRPL][kChunks];
-#pragma unroll
-        for (int r = 0; r < kRPL; ++r) {
-          const int idx = base + g + 8 * r;
-          act[r] = idx < n;
-          id[r] = act[r] ? ids[idx] : 0u;
-          row[r] = p.base + static_cast<uint64_t>(id[r]) * p.stride;
-        }
-#pragma unroll
-        for (int r = 0; r < kRPL; ++r) {
-          const float4 *rp = reinterpret_cast<const float4 *>(row[r]) + m;
-          if (act[r]) {
-#pragma unroll
-            for (int t = 0; t < kChunks; ++t) y[r][t] = rp[8 * t];
-          } else {
-#pragma unroll
-            for (int t = 0; t < kChunks; ++t) y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-        float a[kRPL][4];
-#pragma unroll
-        for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
-        const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
-#pragma unroll
-        for (int t = 0; t < kChunks; ++t) {
-          const float4 x = qp[8 * t];
-#pragma unroll
-          for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
-        }
-#pragma unroll
-        for (int r = 0; r < kRPL; ++r) {
-          if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
-            for (int b = 0; b < nb8; ++b) {
-              const int e = 32 * T + 8 * b + 4 * m;
-              if (act[r]) {
-                accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
-                                *reinterpret_cast<const float4 *>(row[r] + e), a[r][0], a[r][1], a[r][2], a[r][3]);
-              }
-            }
-          }
-          const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
-          if (act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row[r], tail_begin, res, id[r]);
-        }
-      }
+    constexpr int kStep = 8 * RowPass<kChunks>::kR;
+    for (int base = 0; base < n; base += kStep) {
+      RowPass<kChunks> P;
+      issue_rows<kChunks>(p, ids, n, base, P);
+      finish_rows<kIP, kChunks>(p, q, base, P, out);
     }
+    (void)g; (void)m; (void)tail_begin;
   } else {
     for (int base = 0; base < n; base += 8) {
       const int r = base + g;
