@@ -180,9 +180,18 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   hip_check(alaya_amd::search_occupancy(p, fixed + 4096, &vgpr_blocks), "occupancy");
   vgpr_blocks = std::max(1, vgpr_blocks);
   const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
-  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_blocks, want));
-  const size_t budget = kLdsPerCu / blocks > fixed ? kLdsPerCu / blocks - fixed : 0;
+  uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_blocks, want));
   const uint32_t cap = ceil_log2(48ull * ef);
+  if (want > static_cast<uint64_t>(vgpr_blocks)) {
+    // Several queries per resident slot: residency beyond what keeps a table of ~32 ef slots
+    // (load <= ~0.5 at the usual 10-24 ef visited ids) costs more in probes and spills than it
+    // gains (SIFT 1M, 10k queries: 4 waves/SIMD with 8 KB tables beat 5 with 4 KB by ~20 %).
+    const uint32_t tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(32ull * ef)));
+    const bool tc = mode != 2 && fits_compact(tl);
+    const size_t per_block = fixed + (static_cast<size_t>(tc ? 2 : 4) << tl);
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kLdsPerCu / per_block));
+  }
+  const size_t budget = kLdsPerCu / blocks > fixed ? kLdsPerCu / blocks - fixed : 0;
   auto pick = [&](size_t slot_bytes, uint32_t lmax) {
     uint32_t l = 10;
     while (l < lmax && (slot_bytes << (l + 1)) <= budget) ++l;

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--dim", type=int, default=960)
     ap.add_argument("--ef", type=int, default=400)
     ap.add_argument("--hash-log2", type=int, default=0)
+    ap.add_argument("--visited-mode", type=int, default=0, help="0 auto, 1 compact, 2 wide")
+    ap.add_argument("--builder", choices=("host", "gpu"), default="host")
     ap.add_argument("--out", default="")
     ap.add_argument("--workload", choices=("gist", "sq8", "sift"), default="gist",
                     help="sq8: config-5 data (768-d IP, device-built graph), stamped SQ8 traversal")
@@ -48,10 +50,13 @@ def main():
         from workloads.datasets import sift_like
 
         base, queries = sift_like(args.n, args.nq, 128)
-        g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "sift_like_m0")
         dev = ext.DeviceIndex(0)
         dev.set_base(base, 0)
-        dev.set_graph(g)
+        if args.builder == "gpu":
+            dev.build_graph(32, 100, 100, 0, 0, 1)
+        else:
+            g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "sift_like_m0")
+            dev.set_graph(g)
     else:
         base, queries = gist_like(args.n, args.nq, args.dim)
         g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
@@ -60,6 +65,8 @@ def main():
         dev.set_graph(g)
     if args.hash_log2:
         dev.set_hash_log2(args.hash_log2)
+    if args.visited_mode:
+        dev.set_visited_mode(args.visited_mode)
     def plain_search():
         if space:
             return dev.search_sq8(queries, 10, args.ef, 0, None)
