@@ -75,6 +75,8 @@ def parse():
     p.add_argument("--ef", type=int, default=0, help="fixed ef (skip the recall sweep)")
     p.add_argument("--target-recall", type=float, default=0.95)
     p.add_argument("--mode", choices=("shard", "replica"), default="shard")
+    p.add_argument("--no-replica-leg", action="store_true",
+                   help="N>1 shard mode: skip the replica-mode leg reported beside the shard result")
     p.add_argument("--build-threads", type=int, default=0)
     p.add_argument("--builder", choices=("auto", "host", "gpu"), default="auto",
                    help="graph builder: host = HNSWBuilder restated on the host (cached), gpu = the "
@@ -350,13 +352,14 @@ def main():
     cnt_dev = torch.empty((nq, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def launch(ef):
+    def launch(ef, ix=None):
+        ix = index if ix is None else ix
         if use_sq8:  # SQ8 graph search + PyIndex::rerank as batch_search runs it (rerank mode 1)
-            index.search_sq8_device(q_dev.data_ptr(), 0, nq, K, ef, 1, ids_dev.data_ptr(), dists_dev.data_ptr(),
-                                    cnt_dev.data_ptr(), stream.cuda_stream)
+            ix.search_sq8_device(q_dev.data_ptr(), 0, nq, K, ef, 1, ids_dev.data_ptr(), dists_dev.data_ptr(),
+                                 cnt_dev.data_ptr(), stream.cuda_stream)
         else:
-            index.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
-                                cnt_dev.data_ptr(), stream.cuda_stream)
+            ix.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
+                             cnt_dev.data_ptr(), stream.cuda_stream)
 
     def step(ef):
         launch(ef)
@@ -455,6 +458,12 @@ def main():
     units_per_step = nq * (world if (world > 1 and args.mode == "replica") else 1)
     value = units_per_step * args.steps / elapsed
 
+    # ---- replica leg (N>1 shard mode): the whole index on every GPU, each rank its own batch ---
+    replica = None
+    if world > 1 and args.mode == "shard" and not args.no_replica_leg:
+        replica = replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, launch, rank, world,
+                              nq, ids_dev, stream, gt if rank == 0 else None)
+
     # ---- CPU baseline: the reference's coroutine batch_search restated (oracle/) --------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -496,9 +505,60 @@ def main():
         }
         if curve is not None:
             out["config"]["qps_curve"] = curve
+        if replica is not None:
+            out["replica"] = replica
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, launch, rank, world, nq,
+                ids_dev, stream, gt):
+    """SURVEY §8e replica mode, reported beside shard mode: every rank holds the whole index (graph
+    from the device build) and answers its own batch; no collective on the data path.  The
+    operating ef is chosen on rank 0 against the same ground truth.  value = world * nq / step time
+    (max over ranks): "scaling": "weak"."""
+    t = time.time()
+    full = native.DeviceIndex(dev.index)
+    full.set_base(base, metric)
+    full.build_graph(R, args.efc, 100, 0, 0, 1)
+    if use_sq8:
+        mn, mx = native.sq8_train(base)
+        full.set_sq8(native.sq8_encode(base, mn, mx, threads), mn, mx, native.host_sq8_order())
+    log(f"replica leg: device-built full graph in {time.time() - t:.1f}s")
+    sweep = []
+
+    def probe(ef):
+        launch(ef, full)
+        torch.cuda.synchronize()
+        ok = False
+        if rank == 0:
+            r = recall(ids_dev.cpu().numpy(), gt)
+            sweep.append({"ef": ef, "recall": round(r, 4)})
+            ok = r >= args.target_recall
+        flag = torch.tensor([1 if ok else 0], device=dev)
+        dist.broadcast(flag, 0)
+        return bool(flag.item())
+
+    ef = choose_ef(probe)
+    for _ in range(args.warmup):
+        launch(ef, full)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        launch(ef, full)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = el.item()
+    r_at = next((s["recall"] for s in sweep if s["ef"] == ef), None)
+    out = {"value": round(world * nq * args.steps / el, 1), "unit": "queries/s", "scaling": "weak",
+           "ms_per_step": round(el / args.steps * 1e3, 4), "ef_search": ef, "recall_at_10": r_at,
+           "graph_builder": "gpu", "note": "whole index on every GPU, each rank its own batch, no collective"}
+    log("replica leg", out)
+    return out
 
 
 def cpu_baseline(args, graph, base, queries, ef, metric, sq8, device_ids):
