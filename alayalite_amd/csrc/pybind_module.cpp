@@ -143,7 +143,7 @@ class PyIndexInterface {
       {
         py::gil_scoped_release nogil;
         check(alaya_index_set_base(ix_, rows_f32_.data(), n, dim_, metric_code(), nullptr));
-        check(alaya_index_build_graph(ix_, params_.max_nbrs_, ef_construction, 100, 0, 0, 1, &graph_, nullptr));
+        check(alaya_index_build_graph(ix_, params_.max_nbrs_, ef_construction, 100, 0, 0, 2, &graph_, nullptr));
       }
       if (params_.quantization_type_ == QuantizationType::SQ8) {
         train_sq8(num_threads);
@@ -933,7 +933,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("set_base", &DeviceIndex::set_base, py::arg("rows"), py::arg("metric") = 0, py::arg("valid") = py::none())
       .def("set_graph", &DeviceIndex::set_graph)
       .def("build_graph", &DeviceIndex::build_graph, py::arg("R") = 32, py::arg("ef_construction") = 100,
-           py::arg("seed") = 100, py::arg("batch_div") = 0, py::arg("max_batch") = 0, py::arg("refine") = 1)
+           py::arg("seed") = 100, py::arg("batch_div") = 0, py::arg("max_batch") = 0, py::arg("refine") = 2)
       .def("search", &DeviceIndex::search, py::arg("queries"), py::arg("k"), py::arg("ef"))
       .def("search_device", &DeviceIndex::search_device)
       .def("distances", &DeviceIndex::distances)

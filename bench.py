@@ -329,7 +329,7 @@ def main():
     index.set_base(my_base, metric)
     if builder == "gpu":
         t = time.time()
-        graph, bstats = index.build_graph(R, args.efc, 100, 0, 0, 1)
+        graph, bstats = index.build_graph(R, args.efc, 100, 0, 0, 2)
         build_s = time.time() - t
         log(f"device-built graph {my_base.shape} in {build_s:.1f}s ({bstats})")
     else:
@@ -521,7 +521,7 @@ def replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, 
     t = time.time()
     full = native.DeviceIndex(dev.index)
     full.set_base(base, metric)
-    full.build_graph(R, args.efc, 100, 0, 0, 1)
+    full.build_graph(R, args.efc, 100, 0, 0, 2)
     if use_sq8:
         mn, mx = native.sq8_train(base)
         full.set_sq8(native.sq8_encode(base, mn, mx, threads), mn, mx, native.host_sq8_order())

@@ -97,7 +97,7 @@ int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uin
  * defaults 16 / 65536); within a batch every point runs searchBaseLayer + the neighbour heuristic
  * on the device against the graph as it stood before the batch, then reverse edges are merged per
  * destination (append, or prune with the heuristic).  `refine` extra level-0 passes per batch let
- * the batch's points re-select among each other once they are linked in (1 recommended; with
+ * the batch's points re-select among each other once they are linked in (2 recommended; with
  * batch_div = max_batch = 1 and refine = 0 the insertion is sequential, as the reference's).  The result is installed as the index's
  * search graph and a host copy is returned in *out (nullable).  stats (nullable, 8 x u64):
  * batches, kernel launches, list prunes, appended edges, heuristic distances, device time (us),

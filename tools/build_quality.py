@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--efc", type=int, default=100)
     ap.add_argument("--batch-div", type=int, default=0)
     ap.add_argument("--max-batch", type=int, default=0)
+    ap.add_argument("--refine", type=int, default=1)
+    ap.add_argument("--variants", default="", help="extra device builds: 'efc:div:refine;...'")
     ap.add_argument("--host", action="store_true", help="also build on the host (16 threads) for comparison")
     ap.add_argument("--efs", default="40,80,120,200,300,400")
     a = ap.parse_args()
@@ -60,10 +62,17 @@ def main():
     ix = native.DeviceIndex(0)
     ix.set_base(base, metric, None)
     t = time.perf_counter()
-    g, st = ix.build_graph(32, a.efc, 100, a.batch_div, a.max_batch)
+    g, st = ix.build_graph(32, a.efc, 100, a.batch_div, a.max_batch, a.refine)
     wall = time.perf_counter() - t
     print(json.dumps({"builder": "gpu", "n": a.n, "gen": a.gen, "build_s": round(wall, 3), "stats": st,
                       "curve": curve(ix)}), flush=True)
+    for v in filter(None, a.variants.split(";")):
+        efc, bd, rf = (int(x) for x in v.split(":"))
+        t = time.perf_counter()
+        ix.build_graph(32, efc, 100, bd, 0, rf)
+        wall = time.perf_counter() - t
+        print(json.dumps({"builder": f"gpu efc{efc} div{bd} refine{rf}", "n": a.n, "build_s": round(wall, 3),
+                          "curve": curve(ix)}), flush=True)
     if a.host:
         t = time.perf_counter()
         hg = native.Graph.build(base, metric, 32, a.efc, bench.host_threads(), 100)
