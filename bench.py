@@ -264,6 +264,20 @@ def run_flat(args):
         ok += int(set(np.argsort(d)[:K].tolist()) == set(got[qi].tolist()))
     flops = 2.0 * n * nq * dim
     tf = flops / (ms * 1e-3) / 1e12
+    cpu = None
+    if not args.no_cpu_baseline:  # find_exact_gt restated (oracle/), a bounded sample of the queries
+        import oracle
+
+        oracle.build()
+        ct = args.cpu_threads or host_threads()
+        _, t_probe = oracle.exact_gt(base, queries[:ct], K, ct)
+        m = int(min(nq, max(ct, ct * int(20.0 / max(t_probe, 1e-6)))))
+        cpu_ids, sec = oracle.exact_gt(base, queries[:m], K, ct)
+        same = int(sum(set(cpu_ids[i].tolist()) == set(got[i].tolist()) for i in range(m)))
+        cpu = {"value": round(m / sec, 1), "unit": "queries/s", "cores": ct, "kind": "port",
+               "sample": f"{m} of {nq} queries, find_exact_gt restated (l2_sqr AVX2 order + std::sort per query), "
+                         f"queries over {ct} threads; top-{K} sets equal to the device's on {same}/{m}"}
+        log("cpu baseline", cpu)
     out = {
         "metric": "QPS, flat exact k-NN, 1M x 128 L2, 1k queries (BASELINE config 2)",
         "value": round(nq * args.steps / elapsed, 1), "unit": "queries/s", "n_gpus": 1, "steps": args.steps,
@@ -274,7 +288,7 @@ def run_flat(args):
         "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
                      "frac": round(tf / 157.3, 4), "traffic": None, "kernel": "flat_scan_kernel+flat_merge_kernel",
                      "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops},
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
 

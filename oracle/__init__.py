@@ -110,6 +110,8 @@ def lib():
         _lib.orc_updater_remove.argtypes = [p, C.c_uint32]
         _lib.orc_batch_rerank.restype = C.c_double
         _lib.orc_batch_rerank.argtypes = [C.POINTER(OrcIndex), p, C.c_uint64, p, C.c_uint32, C.c_uint32, p, p]
+        _lib.orc_exact_gt.restype = C.c_double
+        _lib.orc_exact_gt.argtypes = [p, C.c_uint64, C.c_uint32, p, C.c_uint64, C.c_uint32, C.c_uint32, p]
         _lib.orc_sq8_fit.argtypes = [p, C.c_uint64, C.c_uint32, p, p]
         _lib.orc_sq8_encode.argtypes = [p, C.c_uint32, p, p, p]
         for name in ("orc_sq8_l2", "orc_sq8_ip"):
@@ -178,6 +180,15 @@ class Pool:
 
     def dist(self, i):
         return lib().orc_pool_dist(self._h, i)
+
+
+def exact_gt(base, queries, k, num_threads=1):
+    """find_exact_gt (evaluate.hpp:29-62) restated; returns (ids[nq, k], seconds)."""
+    b = np.ascontiguousarray(base, np.float32)
+    q = np.ascontiguousarray(queries, np.float32)
+    ids = np.zeros((q.shape[0], k), np.uint32)
+    sec = lib().orc_exact_gt(_ptr(b), b.shape[0], b.shape[1], _ptr(q), q.shape[0], k, num_threads, _ptr(ids))
+    return ids, sec
 
 
 class IndexView:

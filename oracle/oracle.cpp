@@ -593,6 +593,33 @@ void orc_rerank(const orc_index *ix, const float *query, const uint32_t *search_
 
 // The Linux batch path's rerank loop after Scheduler::join (index.hpp:337-345): one thread, query
 // by query.  Returns its seconds (outside the reference's Timer, but part of batch_search).
+double orc_exact_gt(const float *base, uint64_t n, uint32_t dim, const float *queries, uint64_t nq,
+                    uint32_t k, uint32_t num_threads, uint32_t *ids) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool avx2 = orc_cpu_has_avx2_fma() != 0;
+  std::atomic<uint64_t> next{0};
+  auto work = [&]() {
+    std::vector<std::pair<uint32_t, float>> dists;
+    dists.reserve(n);
+    for (;;) {
+      const uint64_t i = next.fetch_add(1);
+      if (i >= nq) break;
+      dists.clear();
+      const float *q = queries + i * dim;
+      for (uint64_t j = 0; j < n; ++j) {
+        const float *row = base + j * dim;
+        dists.emplace_back(static_cast<uint32_t>(j), avx2 ? orc_l2_f32_avx2(q, row, dim) : orc_l2_f32(q, row, dim));
+      }
+      std::sort(dists.begin(), dists.end(), [](const auto &a, const auto &b) { return a.second < b.second; });
+      for (uint32_t j = 0; j < k && j < dists.size(); ++j) ids[i * k + j] = dists[j].first;
+    }
+  };
+  std::vector<std::thread> ts;
+  for (uint32_t t = 0; t < std::max(1u, num_threads); ++t) ts.emplace_back(work);
+  for (auto &t : ts) t.join();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 double orc_batch_rerank(const orc_index *ix, const float *queries, uint64_t nq, const uint32_t *search_ids,
                         uint32_t k, uint32_t ef, uint32_t *ids, float *dists) {
   auto t0 = std::chrono::steady_clock::now();

@@ -127,6 +127,11 @@ int64_t orc_updater_insert(orc_updater *u, const float *search_query, const floa
 void orc_updater_remove(orc_updater *u, uint32_t id);
 
 /* ---- SQ8 ---------------------------------------------------------------------------------- */
+/* find_exact_gt (include/utils/evaluate.hpp:29-62): per query, l2_sqr to every row, std::sort of
+ * (id, dist) by dist, the first k ids.  Queries split over num_threads threads (the reference loops
+ * them on one thread).  Returns the seconds spent (CPU baseline of the flat path, config 2). */
+double orc_exact_gt(const float *base, uint64_t n, uint32_t dim, const float *queries, uint64_t nq,
+                    uint32_t k, uint32_t num_threads, uint32_t *ids);
 void orc_sq8_fit(const float *data, uint64_t n, uint32_t dim, float *min_v, float *max_v);
 void orc_sq8_encode(const float *row, uint32_t dim, const float *min_v, const float *max_v,
                     uint8_t *code);

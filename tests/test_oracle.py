@@ -132,3 +132,15 @@ def test_normalize(orc):
     v = np.array([3.0, 4.0], np.float32)
     n = orc.normalize(v)
     assert np.allclose(n, [0.6, 0.8])
+
+
+def test_exact_gt_restatement(orc):
+    """find_exact_gt (evaluate.hpp:29-62): l2_sqr to every row, sort by distance, first k ids."""
+    rng = np.random.default_rng(11)
+    base = rng.random((2000, 40), dtype=np.float32)
+    q = rng.random((12, 40), dtype=np.float32)
+    ids, sec = orc.exact_gt(base, q, 10, 3)
+    assert sec >= 0
+    for i in range(q.shape[0]):
+        d = np.array([orc.l2(q[i], base[j]) for j in range(base.shape[0])], np.float32)
+        assert set(ids[i].tolist()) == set(np.argsort(d, kind="stable")[:10].tolist())
