@@ -1,0 +1,54 @@
+"""Kernel time on fixed, deterministic (device-built) graphs, for A/B across builds:
+SIFT 1M ef 85 (10k queries), GIST 1M ef 400 (1k), 768-d IP SQ8 1M ef 175 (1k)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from alayalite_amd import _native
+    from workloads.datasets import gist_like, sift_like, text_like
+
+    ext = _native._ext
+    st = torch.cuda.current_stream()
+    for name, gen, nq, ef, metric, sq8 in (("sift", sift_like, 10000, 85, 0, False),
+                                           ("gist", gist_like, 1000, 400, 0, False),
+                                           ("sq8", text_like, 1000, 175, 1, True)):
+        base, q = gen(1_000_000, nq)
+        dev = ext.DeviceIndex(0)
+        dev.set_base(base, metric)
+        dev.build_graph(32, 100, 100, 0, 0, 2)
+        if sq8:
+            mn, mx = ext.sq8_train(base)
+            dev.set_sq8(ext.sq8_encode(base, mn, mx, 16), mn, mx, ext.host_sq8_order())
+        qd = torch.from_numpy(q).cuda()
+        ids = torch.empty((nq, 10), dtype=torch.int32, device="cuda")
+        dd = torch.empty((nq, 10), dtype=torch.float32, device="cuda")
+        cnt = torch.empty((nq, 4), dtype=torch.int32, device="cuda")
+
+        def run():
+            if sq8:
+                dev.search_sq8_device(qd.data_ptr(), 0, nq, 10, ef, 1, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(),
+                                      st.cuda_stream)
+            else:
+                dev.search_device(qd.data_ptr(), nq, 10, ef, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(), st.cuda_stream)
+
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(20):
+            run()
+        e1.record(st)
+        torch.cuda.synchronize()
+        h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
+        print(f"{name}: {e0.elapsed_time(e1) / 20:.4f} ms  ids-hash {h}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
