@@ -26,22 +26,42 @@ def merge_topk(all_ids, all_dists, k: int):
     return torch.gather(ids, 1, o2), torch.gather(d, 1, o2)
 
 
+def pack_candidates(gid, dists):
+    """(global id, f32 distance) -> one int64 whose signed order is (distance asc, id asc):
+    the distance bits mapped to an order-preserving int32 (negatives' magnitude bits flipped,
+    -0.0 folded into +0.0) in the high word, the id (< 2^32) in the low word."""
+    import torch
+
+    bits = (dists.to(torch.float32) + 0.0).contiguous().view(torch.int32).to(torch.int64)
+    skey = torch.where(bits < 0, bits ^ 0x7FFFFFFF, bits)
+    return (skey << 32) | (gid.to(torch.int64) & 0xFFFFFFFF)
+
+
+def unpack_candidates(packed):
+    import torch
+
+    gid = packed & 0xFFFFFFFF
+    skey = packed >> 32
+    bits = torch.where(skey < 0, skey ^ 0x7FFFFFFF, skey).to(torch.int32)
+    return gid, bits.view(torch.float32)
+
+
 def exchange_and_merge(local_ids, local_dists, offset: int, k: int, group=None):
-    """local_ids: [nq, k] shard-local ids (int32/int64 tensor); returns merged global (ids, dists)."""
+    """local_ids: [nq, k] shard-local ids (int32/int64 tensor); returns merged global (ids, dists).
+    One all_gather of packed (distance, id) keys and one sort: the smallest k keys are the top-k
+    by (distance, global id)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     device = local_ids.device
-    gid = local_ids.to(torch.int64) + offset
-    ld = local_dists
+    packed = pack_candidates(local_ids.to(torch.int64) + offset, local_dists)
     if dist.get_backend(group) == "gloo" and device.type != "cpu":  # gloo gathers host tensors
-        gid, ld = gid.cpu(), ld.cpu()
-    g_ids = [torch.empty_like(gid) for _ in range(world)]
-    g_d = [torch.empty_like(ld) for _ in range(world)]
-    dist.all_gather(g_ids, gid, group=group)
-    dist.all_gather(g_d, ld, group=group)
-    ids, d = merge_topk(torch.cat(g_ids, 1), torch.cat(g_d, 1), k)
+        packed = packed.cpu()
+    parts = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(parts, packed, group=group)
+    best = torch.sort(torch.cat(parts, 1), dim=1).values[:, :k]
+    ids, d = unpack_candidates(best)
     return ids.to(device), d.to(device)
 
 

@@ -64,3 +64,20 @@ def test_exchange_and_merge_gloo(tmp_path):
     ref_i, ref_d = merge_reference([p[0] for p in parts], [p[1] for p in parts], [0, 500], 10)
     assert np.array_equal(got["ids"], ref_i)
     assert np.array_equal(got["d"], ref_d)
+
+
+def test_packed_keys_order_like_dist_then_id():
+    """The exchange packs (distance, global id) into one int64 whose order is (dist asc, id asc):
+    negative distances (IP), -0.0 vs +0.0 and ties across ids included; the merge result equals the
+    two-sort merge."""
+    from alayalite_amd.sharded import merge_topk, pack_candidates, unpack_candidates
+
+    rng = np.random.default_rng(3)
+    d = np.concatenate([rng.normal(size=(40, 30)).astype(np.float32), np.zeros((40, 2), np.float32),
+                        np.full((40, 2), -0.0, np.float32), np.full((40, 2), np.inf, np.float32)], 1)
+    d[:, 4] = d[:, 7]
+    ids = rng.integers(0, 2 ** 31 - 1, d.shape).astype(np.int64)
+    dt, it = torch.from_numpy(d), torch.from_numpy(ids)
+    gi, gd = unpack_candidates(torch.sort(pack_candidates(it, dt), 1).values[:, :10])
+    mi, md = merge_topk(it, dt + 0.0, 10)
+    assert torch.equal(gi, mi) and torch.equal(gd.view(torch.int32), (md + 0.0).view(torch.int32))
