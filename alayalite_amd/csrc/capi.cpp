@@ -18,6 +18,7 @@
 #include "graph_update.h"
 #include "hnsw_build.h"
 #include "flat_kernels.h"
+#include <cstdlib>
 #include "search_kernels.h"
 
 using alaya_amd::HostGraph;
@@ -286,6 +287,9 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
   p.stride = ix->stride;
   p.norms = ix->norms.as<float>();
   p.max_norm = ix->max_norm;
+  // bf16 split contraction unless the rows are large enough for bf16(x) to overflow, or
+  // ALAYA_FLAT_F32 is set (the f32-MFMA contraction; both feed the same exact rescoring)
+  p.split = ix->max_norm < 1e18f && std::getenv("ALAYA_FLAT_F32") == nullptr;
   p.queries = d_q;
   p.nq = nq;
   p.q_stride = ix->dim;

@@ -24,6 +24,7 @@ struct FlatParams {
   uint32_t *out_ids;   // nq x k
   float *out_dists;    // nq x k, nullable
   uint32_t *flags;     // nq: 1 = shortlist bound not proven, recompute exhaustively
+  int split;           // 1 = bf16 hi/lo split contraction (3 bf16 MFMAs), 0 = f32 MFMA
   int ablate;          // diagnostics only: 1 = skip candidate handling (MFMA + tile stream only)
   uint32_t *merge_count;  // diagnostics only (nullable): merges per block
 };

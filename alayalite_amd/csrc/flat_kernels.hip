@@ -33,6 +33,17 @@ constexpr int kBuf = 96;     // candidate buffer per query
 constexpr int kTile = 32;    // base rows per LDS tile
 constexpr int kPad = 4;      // LDS row pitch padding (floats)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// Split contraction (kSplit): x = hi + lo + r with hi = bf16(x), lo = bf16(x - hi) (x - hi is exact
+// in f32), |r| <= 2^-16 |x|.  q.b ~= qh.bh + qh.bl + ql.bh: three v_mfma_f32_32x32x16_bf16 per 16 k
+// (products exact in f32) instead of eight v_mfma_f32_32x32x2f32 -- 768 vs 4096 MFMA cycles per
+// 32x32x128 tile.  The dropped terms are bounded by ~3 * 2^-16 |q||b| (flat_merge_kernel's eps).
+__device__ __forceinline__ void split_bf16(float x, __bf16 &hi, __bf16 &lo) {
+  hi = static_cast<__bf16>(x);
+  lo = static_cast<__bf16>(x - static_cast<float>(hi));
+}
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -110,17 +121,21 @@ __device__ __forceinline__ void fold32(float &L, uint32_t &Li, float cd, uint32_
   fold32_sorted(L, Li, cd, ci, col);
 }
 
-template <int K>
+template <int K, bool kSplit>
 __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
-  static_assert(K % 8 == 0 && K <= 256, "K must be a multiple of 8, at most 256");
+  static_assert(K % 16 == 0 && K <= 256, "K must be a multiple of 16, at most 256");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // f32: row pitch K+4 floats.  split: a hi and a lo half-tile of bf16 rows with pitch K+8 (2K+16
+  // bytes, so the 16 rows of a ds_read_b128 group start on distinct 16-byte bank quads).
   constexpr int kPitch = K + kPad;
-  float *tile = reinterpret_cast<float *>(smem);                       // 2 x kTile x kPitch
-  float *nrm = tile + 2 * kTile * kPitch;                               // 2 x kTile
+  constexpr int kBPitch = K + 8;
+  constexpr int kTileWords = kSplit ? kTile * kBPitch : kTile * kPitch;  // 4-byte words per buffer
+  float *tile = reinterpret_cast<float *>(smem);                       // 2 x kTileWords
+  float *nrm = tile + 2 * kTileWords;                                   // 2 x kTile
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
-  float *bd = tile + 2 * kTile * kPitch + 2 * kTile + wave * 32 * kBuf * 2;  // 32 queries x kBuf
+  float *bd = tile + 2 * kTileWords + 2 * kTile + wave * 32 * kBuf * 2;  // 32 queries x kBuf
   uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kBuf);
 
   // XCD-aware block -> (query group, chunk): the query groups of one chunk share an XCD label.
@@ -145,6 +160,20 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       if (qi < p.nq) v = *reinterpret_cast<const float4 *>(qp + s);
       a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
     }
+  }
+  // split: k-step s of lane (col, h) holds query elements h*K/2 + 8s + j, j < 8 (the base fragment
+  // below uses the same map, so the MFMA's k = 8h + j pairs equal elements)
+  bf16x8 ah[kSplit ? K / 16 : 1], al[kSplit ? K / 16 : 1];
+  if constexpr (kSplit) {
+#pragma unroll
+    for (int s = 0; s < K / 16; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 hi, lo;
+        split_bf16(a[8 * s + j], hi, lo);
+        ah[s][j] = hi;
+        al[s][j] = lo;
+      }
   }
   // Shortlists live in registers with the accumulator's layout: register r of half h holds the
   // ascending list of query qloc(r, h), entry (lane & 31).  cnt[r] = buffered candidates of that
@@ -181,11 +210,26 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     }
   };
   auto store_tile = [&](int buf, const float4 (&reg)[kPerThread], const float (&nr)[1]) {
-    float *t = tile + buf * kTile * kPitch;
+    float *t = tile + buf * kTileWords;
 #pragma unroll
     for (int v = 0; v < kPerThread; ++v) {
       const int idx = threadIdx.x + v * 256;
-      if (idx < kVecs) *reinterpret_cast<float4 *>(t + (idx / kVecPerRow) * kPitch + (idx % kVecPerRow) * 4) = reg[v];
+      if (idx < kVecs) {
+        if constexpr (kSplit) {
+          // split once per tile here, not per wave at the fragment reads
+          __bf16 *th = reinterpret_cast<__bf16 *>(t) + (idx / kVecPerRow) * kBPitch + (idx % kVecPerRow) * 4;
+          bf16x4 hv, lv;
+          __bf16 hi, lo;
+          split_bf16(reg[v].x, hi, lo); hv[0] = hi; lv[0] = lo;
+          split_bf16(reg[v].y, hi, lo); hv[1] = hi; lv[1] = lo;
+          split_bf16(reg[v].z, hi, lo); hv[2] = hi; lv[2] = lo;
+          split_bf16(reg[v].w, hi, lo); hv[3] = hi; lv[3] = lo;
+          *reinterpret_cast<bf16x4 *>(th) = hv;
+          *reinterpret_cast<bf16x4 *>(th + kTile * kBPitch) = lv;
+        } else {
+          *reinterpret_cast<float4 *>(t + (idx / kVecPerRow) * kPitch + (idx % kVecPerRow) * 4) = reg[v];
+        }
+      }
     }
     if (threadIdx.x < kTile) nrm[buf * kTile + threadIdx.x] = nr[0];
   };
@@ -201,15 +245,27 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   for (uint64_t row0 = r0; row0 < r1; row0 += kTile) {
     const bool more = row0 + kTile < r1;
     if (more) load_tile(row0 + kTile, stage, stage_n);  // next tile in flight during the MFMAs
-    const float *t = tile + buf * kTile * kPitch + col * kPitch + h * (K / 2);
     f32x16 c = {};
+    if constexpr (kSplit) {
+      const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
 #pragma unroll
-    for (int s = 0; s < K / 2; s += 4) {
-      const float4 bv = *reinterpret_cast<const float4 *>(t + s);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bv.x, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 1], bv.y, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 2], bv.z, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 3], bv.w, c, 0, 0, 0);
+      for (int s = 0; s < K / 16; ++s) {
+        const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * s);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * s);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh, c, 0, 0, 0);
+      }
+    } else {
+      const float *t = tile + buf * kTile * kPitch + col * kPitch + h * (K / 2);
+#pragma unroll
+      for (int s = 0; s < K / 2; s += 4) {
+        const float4 bv = *reinterpret_cast<const float4 *>(t + s);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bv.x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 1], bv.y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 2], bv.z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 3], bv.w, c, 0, 0, 0);
+      }
     }
     const float bn = nrm[buf * kTile + col];
     const uint32_t rid = static_cast<uint32_t>(row0 + col);
@@ -447,10 +503,15 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
       const uint64_t mk = __ballot(lane < kL && rank == p.k - 1);
       kth_d = mk ? __shfl(dv, __ffsll(static_cast<unsigned long long>(mk)) - 1) : FLT_MAX;
     }
-    const float gam = 2.0f * static_cast<float>(p.stride) * 5.9604645e-8f;
+    // split contraction: the f32 accumulation covers 3K terms of total magnitude <= 1.02 |q||b|
+    // (gamma x 3.1), and the dropped terms (ql.bl and the two split residuals) add
+    // <= 3.02 * 2^-16 |q||b| to C, i.e. twice that to the distance; 1e-30 covers bf16 lo parts
+    // flushed as denormals.
+    const float gam = 2.0f * static_cast<float>(p.stride) * 5.9604645e-8f * (p.split ? 3.1f : 1.0f);
     const float qnorm = sqrtf(qn);
     const float bmax = p.max_norm;
-    const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax);
+    const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax) +
+                      (p.split ? 2.0f * 3.05f * 1.5258789e-5f * qnorm * bmax + 1e-30f : 0.0f);
     const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     wave_fence();
@@ -472,7 +533,8 @@ __global__ void row_norms_kernel(const float *base, uint64_t n, uint32_t stride,
 
 template <int K>
 size_t scan_lds() {
-  return (2 * kTile * (K + kPad) + 2 * kTile) * 4 + 4 * (32 * kBuf * 8);
+  // the split tile (hi + lo bf16 rows, pitch K+8) is 4 bytes per row larger than the f32 tile
+  return (2 * kTile * (K + 8) + 2 * kTile) * 4 + 4 * (32 * kBuf * 8);
 }
 
 }  // namespace
@@ -503,7 +565,10 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
   if (lds == 0) return hipErrorInvalidValue;
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
-    hipLaunchKernelGGL(flat_scan_kernel<K>, dim3(blocks), dim3(256), lds, s, p);               \
+    if (p.split)                                                                               \
+      hipLaunchKernelGGL((flat_scan_kernel<K, true>), dim3(blocks), dim3(256), lds, s, p);     \
+    else                                                                                       \
+      hipLaunchKernelGGL((flat_scan_kernel<K, false>), dim3(blocks), dim3(256), lds, s, p);    \
     break;
   switch (p.stride) {
     ALAYA_FLAT(32) ALAYA_FLAT(64) ALAYA_FLAT(96) ALAYA_FLAT(128) ALAYA_FLAT(160) ALAYA_FLAT(192)

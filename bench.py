@@ -287,7 +287,13 @@ def run_flat(args):
                    "flagged_queries": n_flag, "exact_vs_f64_sample": f"{ok}/{len(sample)}"},
         "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
                      "frac": round(tf / 157.3, 4), "traffic": None, "kernel": "flat_scan_kernel+flat_merge_kernel",
-                     "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops},
+                     "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops,
+                     # the default contraction issues 3 bf16 MFMAs per f32 product (hi/lo split):
+                     # its own ceiling is the 2.5 PF bf16 peak / 3, which the scan is far from --
+                     # candidate handling, not the MFMA pipe, sets the time
+                     "contraction": "f32" if os.environ.get("ALAYA_FLAT_F32") else "bf16x3",
+                     "split_ceiling": None if os.environ.get("ALAYA_FLAT_F32") else 833.3,
+                     "split_frac": None if os.environ.get("ALAYA_FLAT_F32") else round(tf / 833.3, 4)},
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -8,6 +8,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["split", "f32"], autouse=True)
+def flat_mode(request, monkeypatch):
+    """Both shortlist contractions: the bf16 hi/lo split (default) and the f32 MFMA
+    (ALAYA_FLAT_F32).  The exact rescoring and the bound check make the answer identical."""
+    if request.param == "f32":
+        monkeypatch.setenv("ALAYA_FLAT_F32", "1")
+    else:
+        monkeypatch.delenv("ALAYA_FLAT_F32", raising=False)
+    return request.param
+
+
 def _exact(orc, base, q, k):
     lib = orc.lib()
     out_i = np.zeros((len(q), k), np.uint32)
@@ -27,6 +38,22 @@ def test_flat_exact(native, orc, n, d, nq):
     rng = np.random.default_rng(n + d)
     base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
     q = np.ascontiguousarray(rng.random((nq, d), dtype=np.float32))
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    ref_i, ref_d = _exact(orc, base, q, 10)
+    assert np.array_equal(ids, ref_i)
+    assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+    assert redo == 0  # the shortlist bound is proven on every query of continuous data
+
+
+@pytest.mark.parametrize("scale,shift", [(1e3, 0.0), (1e-3, 0.0), (1.0, -0.5), (1e-20, 1e-21)])
+def test_flat_exact_scaled(native, orc, scale, shift):
+    """Signed, large and tiny magnitudes (bf16 lo parts in the denormal range at 1e-20): the
+    split contraction's error bound scales with |q||b|, so the answer stays exact."""
+    rng = np.random.default_rng(7)
+    base = np.ascontiguousarray((rng.standard_normal((3000, 96)) * scale + shift).astype(np.float32))
+    q = np.ascontiguousarray((rng.standard_normal((40, 96)) * scale + shift).astype(np.float32))
     dev = native.DeviceIndex(0)
     dev.set_base(base, 0)
     ids, dists, redo = dev.flat_search(q, 10)
