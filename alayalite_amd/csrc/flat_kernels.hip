@@ -181,6 +181,7 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   float ld[16], tau[16];
   uint32_t li[16];
   int cnt[16];
+  uint32_t full = 0, nonempty = 0;  // registers whose buffer holds >= kTile / > 0 candidates (uniform)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     ld[r] = FLT_MAX;
@@ -282,7 +283,10 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       __syncthreads();
       continue;
     }
-    // append candidates below each query's threshold (counts stay in registers)
+    // append candidates below each query's threshold (counts stay in registers).  The common case
+    // per register is fma, compare, one uniform branch: the bookkeeping for folds (`full`,
+    // `nonempty`, `need`) changes only when a register takes an append, so it lives inside that
+    // branch, in scalar masks carried across tiles.
     const uint64_t ta = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t need = 0;
 #pragma unroll
@@ -290,7 +294,7 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
       const float dv = fmaf(-2.0f, c[r], bn);
       const bool pass = live && dv < tau[r];
-      const uint64_t mk = __ballot(pass);
+      const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
       if (mk) {
         const uint32_t hm = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
         if (pass) {
@@ -299,23 +303,19 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
           bi[qloc * kBuf + pos] = rid;
         }
         cnt[r] += __popc(hm);
-      }
-      if (__ballot(cnt[r] > kBuf - kTile || (!more && cnt[r] > 0))) need |= 1u << r;
-    }
-    // Smoothing: besides the folds that are due, fold the fullest buffer once it holds a full
-    // batch.  One fold per wave per tile keeps the four waves' fold work level between barriers.
-    if (need == 0) {
-      int best = 0, best_r = 0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = max(__builtin_amdgcn_readlane(cnt[r], 0), __builtin_amdgcn_readlane(cnt[r], 32));
-        if (m > best) {
-          best = m;
-          best_r = r;
+        nonempty |= 1u << r;
+        if (__builtin_amdgcn_ballot_w64(cnt[r] >= kTile)) {
+          full |= 1u << r;
+          if (__builtin_amdgcn_ballot_w64(cnt[r] > kBuf - kTile)) need |= 1u << r;  // could overflow next tile
         }
       }
-      if (best >= kTile) need = 1u << best_r;
     }
+    if (!more) need |= nonempty;  // last tile: fold everything buffered
+    // Smoothing: besides the folds that are due, fold one buffer that holds a full batch.  One fold
+    // per wave per tile keeps the four waves' fold work level between barriers.
+    if (need == 0 && full) need = 1u << __builtin_ctz(full);
+    full &= ~need;
+    nonempty &= ~need;
     if (p.ablate == 2) {  // diagnostics: appends only, buffers dropped instead of folded
 #pragma unroll
       for (int r = 0; r < 16; ++r)
