@@ -57,14 +57,32 @@ __device__ __forceinline__ bool before(float da, uint32_t ta, float db, uint32_t
   return da < db || (da == db && ta < tb);
 }
 
-// ds_swizzle in bit mode stays inside each 32-lane half: source lane = ((l & 0x1f) | or) ^ xor.
+// Lane xor within each 32-lane half.  xor 1/2: DPP quad_perm; xor 8: DPP row_ror:8 (rows of 16);
+// xor 4: row_ror:12 or row_ror:4 by lane bit 2 (row_ror:n reads lane (l - n) mod 16 of the row) -- all VALU, no LDS-pipeline round trip.  xor 16 and
+// the 31-reversal: bit-mode ds_swizzle (source lane = ((l & 0x1f) | or) ^ xor, inside the half).
+template <int kXor>
+__device__ __forceinline__ int xor_lane(int v) {
+  if constexpr (kXor == 1) {
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (kXor == 2) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (kXor == 8) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (kXor == 4) {
+    const int up = __builtin_amdgcn_update_dpp(0, v, 0x12C, 0xF, 0xF, false);    // row_ror:12 (l + 4)
+    const int down = __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4  (l - 4)
+    return (__lane_id() & 4) ? down : up;
+  } else {
+    return __builtin_amdgcn_ds_swizzle(v, 0x1f | (kXor << 10));
+  }
+}
 template <int kXor>
 __device__ __forceinline__ float swz_f(float v) {
-  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1f | (kXor << 10)));
+  return __int_as_float(xor_lane<kXor>(__float_as_int(v)));
 }
 template <int kXor>
 __device__ __forceinline__ uint32_t swz_u(uint32_t v) {
-  return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x1f | (kXor << 10)));
+  return static_cast<uint32_t>(xor_lane<kXor>(static_cast<int>(v)));
 }
 __device__ __forceinline__ float lane31_of_half(float v) {
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 31 << 5));
