@@ -328,19 +328,22 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
         }
       }
     }
-    if (!more) need |= nonempty;  // last tile: fold everything buffered
-    // Smoothing: besides the folds that are due, fold one buffer that holds a full batch.  One fold
-    // per wave per tile keeps the four waves' fold work level between barriers.
+    // A fold round takes the newest 32 entries of a buffer (it is a stack), so a round costs the
+    // same wherever it happens.  Due rounds: buffers that could overflow on the next tile (one round
+    // brings > 64 down to <= 64).  Smoothing: otherwise one round of a buffer holding a full batch.
+    // At most ~one round per wave per tile keeps the four waves level between barriers.  The last
+    // tile drains every buffer.
+    if (!more) need |= nonempty;
     if (need == 0 && full) need = 1u << __builtin_ctz(full);
-    full &= ~need;
-    nonempty &= ~need;
     if (p.ablate == 2) {  // diagnostics: appends only, buffers dropped instead of folded
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         if (need & (1u << r)) cnt[r] = 0;
+      full &= ~need;
+      nonempty &= ~need;
       need = 0;
     }
-    // Fold the buffers that could overflow on the next tile into their shortlists.  One copy of the
+    // Fold rounds for the registers in `need`.  One copy of the
     // fold body (a uniform loop over `need`, the register picked by value): unrolling it per
     // register would put ~48 KB of code in the loop and thrash the instruction cache.
     const uint64_t tf = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
@@ -362,23 +365,27 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
           }
         }
         const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int cmax = max(__builtin_amdgcn_readlane(cr, 0), __builtin_amdgcn_readlane(cr, 32));
-        for (int b0 = 0; b0 < cmax; b0 += 32) {
+        do {  // one round; the last tile repeats until the buffer is empty
+          const int start = max(cr - 32, 0);  // uniform per half
           float cd = FLT_MAX;
           uint32_t ci = 0xffffffffu;
-          if (b0 + col < cr) {
-            cd = bd[qloc * kBuf + b0 + col];
-            ci = bi[qloc * kBuf + b0 + col];
+          if (start + col < cr) {
+            cd = bd[qloc * kBuf + start + col];
+            ci = bi[qloc * kBuf + start + col];
           }
           fold32(L, Li, cd, ci, col);
-        }
+          cr = start;
+        } while (!more && __builtin_amdgcn_ballot_w64(cr > 0));
+        if (__builtin_amdgcn_ballot_w64(cr >= kTile)) full |= 1u << r;
+        else full &= ~(1u << r);
+        if (!__builtin_amdgcn_ballot_w64(cr > 0)) nonempty &= ~(1u << r);
         const float th = lane31_of_half(L);
 #pragma unroll
         for (int r2 = 0; r2 < 16; ++r2) {
           if (r2 == r) {
             ld[r2] = L;
             li[r2] = Li;
-            cnt[r2] = 0;
+            cnt[r2] = cr;
             tau[r2] = th;
           }
         }
