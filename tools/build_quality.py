@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--efc", type=int, default=100)
     ap.add_argument("--batch-div", type=int, default=0)
     ap.add_argument("--max-batch", type=int, default=0)
-    ap.add_argument("--refine", type=int, default=1)
+    ap.add_argument("--refine", type=int, default=2)  # the library default (Index.fit(builder="gpu"))
     ap.add_argument("--variants", default="", help="extra device builds: 'efc:div:refine;...'")
     ap.add_argument("--host", action="store_true", help="also build on the host (16 threads) for comparison")
     ap.add_argument("--efs", default="40,80,120,200,300,400")
