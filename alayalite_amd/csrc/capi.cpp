@@ -113,7 +113,7 @@ struct alaya_index {
   uint32_t code_stride = 0;
   DevBuf codes, sq_min, sq_max, rr_q_buf, sq_ids, sq_d;
   // flat path
-  DevBuf norms, cand_d, cand_i, flag_buf, iota;
+  DevBuf norms, cand_d, cand_i, flat_tau, flag_buf, iota;
   bool norms_ready = false;
   float max_norm = 0.f;
   // scratch
@@ -274,6 +274,43 @@ void ensure_norms(alaya_index *ix, hipStream_t stream) {
   ix->norms_ready = true;
 }
 
+// Base chunks per query group: enough blocks to cover the CUs, each chunk >= 64 rows.
+int flat_chunks(alaya_index *ix, int nqg, uint64_t rows) {
+  int chunks = (ix->num_cus + nqg - 1) / nqg;
+  chunks = std::max(8, (chunks + 7) / 8 * 8);
+  const uint64_t max_chunks = std::max<uint64_t>(8, (rows / 64) / 8 * 8);
+  return static_cast<int>(std::min<uint64_t>(chunks, max_chunks));
+}
+
+// Prescan: the same scan over rows 0, S, 2S, ... (S = ALAYA_FLAT_PRESCAN; default 0 = off: on
+// config 2 it cuts fold rounds 846 -> 302 per block but costs more than it saves),
+// then per query the sample's 32nd-best approximate distance as every chunk's starting threshold.
+// The sample's 32nd is about the whole base's (32 S)-th, so the full scan appends ~S candidates
+// per (query, chunk) instead of ~32 (1 + ln(chunk rows / 32)).  Results are unchanged: the
+// threshold only rejects rows that cannot reach the merged 32, and the merge's bound uses it.
+void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStream_t s) {
+  const char *env = std::getenv("ALAYA_FLAT_PRESCAN");
+  const uint64_t step = env ? std::strtoull(env, nullptr, 10) : 0;
+  if (step < 2 || p.n / step < 1024) return;
+  alaya_amd::FlatParams q = p;
+  q.n = (p.n + step - 1) / step;
+  q.row_step = static_cast<uint32_t>(step);
+  const int nqg = static_cast<int>((p.nq + 127) / 128);
+  q.n_chunks = flat_chunks(ix, nqg, q.n);  // <= p.n_chunks: the candidate buffers fit
+  q.tau_init = nullptr;
+  q.out_ids = nullptr;
+  q.out_dists = nullptr;
+  q.flags = nullptr;
+  q.merge_count = nullptr;
+  q.ablate = 0;
+  ix->flat_tau.reserve(p.nq * 4);
+  q.tau_out = ix->flat_tau.as<float>();
+  hip_check(alaya_amd::launch_flat_scan(q, nqg * q.n_chunks, s), "flat prescan");
+  hip_check(alaya_amd::launch_flat_threshold(q, s), "flat threshold");
+  p.tau_init = q.tau_out;
+  (void)blocks;
+}
+
 alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t *d_ids,
                                   float *d_dists, uint32_t *d_flags, int *blocks) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
@@ -294,11 +331,9 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
   p.nq = nq;
   p.q_stride = ix->dim;
   const int nqg = static_cast<int>((nq + 127) / 128);
-  int chunks = (ix->num_cus + nqg - 1) / nqg;
-  chunks = std::max(8, (chunks + 7) / 8 * 8);
-  const uint64_t max_chunks = std::max<uint64_t>(8, (ix->n / 64) / 8 * 8);
-  chunks = static_cast<int>(std::min<uint64_t>(chunks, max_chunks));
+  const int chunks = flat_chunks(ix, nqg, ix->n);
   p.n_chunks = chunks;
+  p.row_step = 1;
   const size_t cand = static_cast<size_t>(chunks) * nq * alaya_amd::flat_shortlist();
   ix->cand_d.reserve(cand * 4);
   ix->cand_i.reserve(cand * 4);
@@ -1253,6 +1288,7 @@ int alaya_index_flat_diag(alaya_index *ix, const float *d_queries, uint64_t nq, 
     ensure_norms(ix, s);
     int blocks = 0;
     alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
+    flat_prescan(ix, p, &blocks, s);
     p.ablate = ablate;
     p.merge_count = d_merge_count;
     hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
@@ -1270,6 +1306,7 @@ int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint
     ensure_norms(ix, s);
     int blocks = 0;
     alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
+    flat_prescan(ix, p, &blocks, s);
     hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
     hip_check(alaya_amd::launch_flat_merge(p, s), "flat merge");
   });
@@ -1292,6 +1329,7 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
     int blocks = 0;
     alaya_amd::FlatParams p = flat_params(ix, ix->q_buf.as<float>(), nq, k, ix->id_buf.as<uint32_t>(),
                                           ix->dist_buf.as<float>(), ix->flag_buf.as<uint32_t>(), &blocks);
+    flat_prescan(ix, p, &blocks, ix->stream);
     hip_check(alaya_amd::launch_flat_scan(p, blocks, ix->stream), "flat scan");
     hip_check(alaya_amd::launch_flat_merge(p, ix->stream), "flat merge");
     std::vector<uint32_t> flags(nq);

@@ -24,6 +24,10 @@ struct FlatParams {
   uint32_t *out_ids;   // nq x k
   float *out_dists;    // nq x k, nullable
   uint32_t *flags;     // nq: 1 = shortlist bound not proven, recompute exhaustively
+  uint32_t row_step;   // scan rows 0, row_step, 2*row_step, ... (n counts scanned rows); 1 = all
+  const float *tau_init;  // nq per-query starting thresholds (nullable = FLT_MAX): the prescan's
+                          // 32nd-best over a row sample, nudged up one ulp (see flat_kernels.hip)
+  float *tau_out;      // threshold kernel output (nq)
   int split;           // 1 = bf16 hi/lo split contraction (3 bf16 MFMAs), 0 = f32 MFMA
   int ablate;          // diagnostics only: 1 = skip candidate handling (MFMA + tile stream only)
   uint32_t *merge_count;  // diagnostics only (nullable): merges per block
@@ -34,5 +38,6 @@ size_t flat_scan_lds(uint32_t stride);
 hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, float *norms, hipStream_t s);
 hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s);
 hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s);
+hipError_t launch_flat_threshold(const FlatParams &p, hipStream_t s);
 
 }  // namespace alaya_amd

@@ -171,13 +171,13 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   float a[K / 2];
   {
     const uint64_t qi = q0 + col;
-    const float *qp = p.queries + qi * p.q_stride + h * (K / 2);
+    // elements past dim are zero (the query rows are dim apart, not stride apart: reading past dim
+    // would take the next query's values or, for the last query, bytes past the buffer -- finite or
+    // not, and Inf/NaN times the base's zero padding is NaN); scalar loads, once per kernel
+    const uint32_t e0 = h * (K / 2);
+    const float *qp = p.queries + qi * p.q_stride;
 #pragma unroll
-    for (int s = 0; s < K / 2; s += 4) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (qi < p.nq) v = *reinterpret_cast<const float4 *>(qp + s);
-      a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
-    }
+    for (int s = 0; s < K / 2; ++s) a[s] = (qi < p.nq && e0 + s < p.dim) ? qp[e0 + s] : 0.f;
   }
   // split: k-step s of lane (col, h) holds query elements h*K/2 + 8s + j, j < 8 (the base fragment
   // below uses the same map, so the MFMA's k = 8h + j pairs equal elements)
@@ -204,7 +204,8 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   for (int r = 0; r < 16; ++r) {
     ld[r] = FLT_MAX;
     li[r] = 0xffffffffu;
-    tau[r] = FLT_MAX;
+    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    tau[r] = (p.tau_init && qi < p.nq) ? p.tau_init[qi] : FLT_MAX;
     cnt[r] = 0;
   }
 
@@ -219,13 +220,14 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       reg[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (idx < kVecs) {
         const uint64_t row = row0 + idx / kVecPerRow;
-        if (row < r1) reg[v] = *reinterpret_cast<const float4 *>(p.base + row * p.stride + (idx % kVecPerRow) * 4);
+        if (row < r1)
+          reg[v] = *reinterpret_cast<const float4 *>(p.base + row * p.row_step * p.stride + (idx % kVecPerRow) * 4);
       }
     }
     nr[0] = 0.f;
     if (threadIdx.x < kTile) {
       const uint64_t row = row0 + threadIdx.x;
-      nr[0] = row < r1 ? p.norms[row] : FLT_MAX;
+      nr[0] = row < r1 ? p.norms[row * p.row_step] : FLT_MAX;
     }
   };
   auto store_tile = [&](int buf, const float4 (&reg)[kPerThread], const float (&nr)[1]) {
@@ -287,7 +289,7 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       }
     }
     const float bn = nrm[buf * kTile + col];
-    const uint32_t rid = static_cast<uint32_t>(row0 + col);
+    const uint32_t rid = static_cast<uint32_t>((row0 + col) * p.row_step);
     const bool live = row0 + col < r1;
     if (p.ablate == 1) {  // diagnostics: keep the accumulator live, skip the candidate path
       float sink = 0.f;
@@ -493,7 +495,10 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
       li[lane] = Li;
     }
     wave_fence();
-    const float cutoff = ld[kL - 1];  // every row outside the shortlist has approx >= cutoff
+    // Every row outside the shortlist has approx >= cutoff: it was either displaced by 32 closer
+    // entries of its chunk or rejected against a threshold that never dropped below
+    // min(its chunk's final 32nd, the prescan threshold).
+    const float cutoff = fminf(ld[kL - 1], p.tau_init ? p.tau_init[qi] : FLT_MAX);
     // exact distances of the shortlist (8 lanes per row, 8 rows per pass)
     const int g = lane >> 3, m = lane & 7;
     for (int base = 0; base < kL; base += 8) {
@@ -540,6 +545,33 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
     const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     wave_fence();
+  }
+}
+
+// Prescan threshold: one wave per query folds the chunk shortlists of a scan over a row sample and
+// keeps the 32nd-best approximate distance T, written as nextafter(T, +inf): the scan's strict
+// `d < tau` then admits every row with d <= T, so the sample's 32 best rows re-enter the full scan
+// and the merged shortlist always holds 32 entries at or below T.
+__global__ void __launch_bounds__(64) flat_threshold_kernel(FlatParams p) {
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
+    float L = FLT_MAX;
+    uint32_t Li = 0xffffffffu;
+    for (int c0 = 0; c0 < p.n_chunks; c0 += 2) {
+      const int chunk = c0 + h;
+      float cd = FLT_MAX;
+      uint32_t ci = 0xffffffffu;
+      if (chunk < p.n_chunks) {
+        const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
+        cd = p.cand_d[o];
+        ci = p.cand_i[o];
+      }
+      fold32_sorted(L, Li, cd, ci, col);
+    }
+    fold32_sorted(L, Li, __shfl_xor(L, 32), __shfl_xor(Li, 32), col);
+    const float th = __shfl(L, kL - 1);
+    if (lane == 0) p.tau_out[qi] = th == FLT_MAX ? FLT_MAX : nextafterf(th, FLT_MAX);
   }
 }
 
@@ -601,6 +633,12 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
     default: return hipErrorInvalidValue;
   }
 #undef ALAYA_FLAT
+  return hipGetLastError();
+}
+
+hipError_t launch_flat_threshold(const FlatParams &p, hipStream_t s) {
+  const int grid = static_cast<int>(p.nq < 4096 ? p.nq : 4096);
+  hipLaunchKernelGGL(flat_threshold_kernel, dim3(grid), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 

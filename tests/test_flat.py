@@ -8,14 +8,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["split", "f32"], autouse=True)
+@pytest.fixture(params=["split", "f32", "split-prescan2", "f32-prescan3"], autouse=True)
 def flat_mode(request, monkeypatch):
     """Both shortlist contractions: the bf16 hi/lo split (default) and the f32 MFMA
-    (ALAYA_FLAT_F32).  The exact rescoring and the bound check make the answer identical."""
-    if request.param == "f32":
+    (ALAYA_FLAT_F32).  The exact rescoring and the bound check make the answer identical.
+    The prescan (a scan over every S-th row that seeds each chunk's threshold; off by default,
+    ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes."""
+    monkeypatch.delenv("ALAYA_FLAT_F32", raising=False)
+    monkeypatch.delenv("ALAYA_FLAT_PRESCAN", raising=False)
+    if request.param.startswith("f32"):
         monkeypatch.setenv("ALAYA_FLAT_F32", "1")
-    else:
-        monkeypatch.delenv("ALAYA_FLAT_F32", raising=False)
+    if "prescan" in request.param:
+        monkeypatch.setenv("ALAYA_FLAT_PRESCAN", request.param[-1])
     return request.param
 
 
