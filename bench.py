@@ -264,6 +264,13 @@ def run_flat(args):
         ok += int(set(np.argsort(d)[:K].tolist()) == set(got[qi].tolist()))
     flops = 2.0 * n * nq * dim
     tf = flops / (ms * 1e-3) / 1e12
+    # HBM traffic of the scan from the committed PMC passes on this workload (tools/run_pmc_flat.sh)
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r01", "traffic_flat.json")
+    if os.path.exists(tpath):
+        t = json.load(open(tpath))
+        if t.get("config", {}).get("n_base") == n and t["config"].get("n_queries") == nq and t["config"].get("dim") == dim:
+            traffic = t
     cpu = None
     if not args.no_cpu_baseline:  # find_exact_gt restated (oracle/), a bounded sample of the queries
         import oracle
@@ -286,7 +293,12 @@ def run_flat(args):
         "config": {"workload": f"flat-{n // 1000}k-{dim}-l2-{nq}q", "n_base": n, "n_queries": nq, "dim": dim, "k": K,
                    "flagged_queries": n_flag, "exact_vs_f64_sample": f"{ok}/{len(sample)}"},
         "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
-                     "frac": round(tf / 157.3, 4), "traffic": None, "kernel": "flat_scan_kernel+flat_merge_kernel",
+                     "frac": round(tf / 157.3, 4),
+                     "traffic": round(traffic["traffic_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1) if traffic else None,
+                     "traffic_unit": "GB/s (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE of flat_scan_kernel)",
+                     "traffic_bytes_per_launch": int(traffic["traffic_bytes_per_launch"]) if traffic else None,
+                     "traffic_source": "profiles/r01/traffic_flat.json" if traffic else None,
+                     "kernel": "flat_scan_kernel+flat_merge_kernel",
                      "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops,
                      # the default contraction issues 3 bf16 MFMAs per f32 product (hi/lo split):
                      # its own ceiling is the 2.5 PF bf16 peak / 3, which the scan is far from --

@@ -4,7 +4,8 @@ record bench.py reports as roofline.traffic.
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KB) counts 128 B requests as 64 B for
 wide coalesced reads -> bytes_read = 2 * FETCH_SIZE * 1024 (cross-checked: TCC_EA0_RDREQ_sum * 64
 equals FETCH_SIZE * 1024 when TCC_EA0_RDREQ_32B_sum == 0).  WRITE_SIZE (KB) is taken as is.
-usage: python tools/pmc_summary.py gpurun_out profiles/r01/traffic.json
+usage: python tools/pmc_summary.py gpurun_out profiles/r01/traffic.json [flat]
+  (flat: tools/run_pmc_flat.sh's flat_scan_kernel passes; algorithmic bytes = the base read once)
 """
 
 import csv
@@ -22,22 +23,27 @@ def per_launch(path, kernel="hnsw_search_kernel"):
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
 
-def main(src, dst):
+def main(src, dst, mode="hnsw"):
     c = {}
     launches = {}
-    for f in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
-        v, n = per_launch(f)
+    prefix, kernel = ("pmcf_", "flat_scan_kernel") if mode == "flat" else ("pmc_", "hnsw_search_kernel")
+    for f in glob.glob(os.path.join(src, prefix + "*", "run_counter_collection.csv")):
+        v, n = per_launch(f, kernel)
         c.update(v)
         launches.update(n)
-    cfg = json.load(open(os.path.join(src, "pmc_FETCH_SIZE.json")))
+    cfg = json.load(open(os.path.join(src, prefix + "FETCH_SIZE.json")))
     read_b = 2.0 * c["FETCH_SIZE"] * 1024.0
     write_b = c.get("WRITE_SIZE", 0.0) * 1024.0
-    alg = cfg["roofline"]["algorithmic_bytes_per_launch"]
+    if mode == "flat":  # the base and the queries read once, the chunk shortlists written once
+        cf = cfg["config"]
+        alg = 4.0 * cf["dim"] * (cf["n_base"] + cf["n_queries"]) + 4.0 * cf["n_base"]
+    else:
+        alg = cfg["roofline"]["algorithmic_bytes_per_launch"]
     hit = c.get("TCC_HIT_sum", 0.0)
     miss = c.get("TCC_MISS_sum", 0.0)
     out = {
-        "kernel": "hnsw_search_kernel",
-        "config": {k: cfg["config"][k] for k in ("n_base", "n_queries", "dim", "k", "ef_search")},
+        "kernel": kernel,
+        "config": {k: cfg["config"][k] for k in ("n_base", "n_queries", "dim", "k", "ef_search") if k in cfg["config"]},
         "launches_per_pass": launches,
         "counters_per_launch": c,
         "hbm_read_bytes_per_launch": read_b,
@@ -46,7 +52,8 @@ def main(src, dst):
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read_b + write_b) / alg,
         "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
-        "rdreq_x64_over_fetch": (c.get("TCC_EA0_RDREQ_sum", 0.0) * 64.0) / (c["FETCH_SIZE"] * 1024.0),
+        "rdreq_x64_over_fetch": (c.get("TCC_EA0_RDREQ_sum", 0.0) * 64.0) / (c["FETCH_SIZE"] * 1024.0)
+        if "TCC_EA0_RDREQ_sum" in c else None,
         "profiled_kernel_ms": cfg["roofline"]["kernel_ms"],
     }
     os.makedirs(os.path.dirname(dst), exist_ok=True)
@@ -55,4 +62,4 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
