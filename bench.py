@@ -2,7 +2,7 @@
 
 One step = one device batch_search of the 1k-query batch at the operating-point ef: the smallest
 ef reaching recall@10 >= 0.95 against exact ground truth, bracketed by the reference's sweep
-{10,20,40,60,80,120,200,400,600,800} and narrowed by bisection to ~5%.  The CPU baseline runs at
+{10,20,40,60,80,120,200,400,600,800} and narrowed by bisection to ~1%.  The CPU baseline runs at
 the same ef.  Inputs (rows, graph, queries) are resident in HBM before the timed region.
 
 N > 1 (torchrun, one rank per GPU):
@@ -191,7 +191,7 @@ def pmc_traffic(cfg):
 def choose_ef(probe):
     """Smallest ef reaching the recall target: the reference's ef sweep (config.yml:21) brackets
     it, then bisection between the last failing and the first passing sweep point narrows it to
-    ~5% (recall is monotone in ef up to noise; the chosen ef is one that was measured to pass)."""
+    ~1% (recall is monotone in ef up to noise; the chosen ef is one that was measured to pass)."""
     lo = 0
     for ef in EF_SWEEP:
         if probe(ef):
@@ -202,7 +202,7 @@ def choose_ef(probe):
         return EF_SWEEP[-1]
     if lo == 0:
         return hi
-    while hi - lo > max(1, lo // 20):
+    while hi - lo > max(1, lo // 100):
         mid = (lo + hi) // 2
         if probe(mid):
             hi = mid

@@ -21,7 +21,7 @@ def test_choose_ef_brackets_then_bisects():
         return ef >= 333
 
     ef = bench.choose_ef(probe)
-    assert ef >= 333 and ef - 333 <= max(1, 200 // 20) + 1
+    assert ef >= 333 and ef - 333 <= max(1, 200 // 100) + 1
     assert seen[:8] == [10, 20, 40, 60, 80, 120, 200, 400]
     assert bench.choose_ef(lambda ef: True) == 10
     assert bench.choose_ef(lambda ef: False) == 800
