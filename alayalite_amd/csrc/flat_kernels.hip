@@ -291,6 +291,7 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     const float bn = nrm[buf * kTile + col];
     const uint32_t rid = static_cast<uint32_t>((row0 + col) * p.row_step);
     const bool live = row0 + col < r1;
+    const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
     if (p.ablate == 1) {  // diagnostics: keep the accumulator live, skip the candidate path
       float sink = 0.f;
 #pragma unroll
@@ -313,8 +314,10 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     for (int r = 0; r < 16; ++r) {
       const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
       const float dv = fmaf(-2.0f, c[r], bn);
-      const bool pass = live && dv < tau[r];
-      const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+      // the compare's lane mask straight from v_cmp (llvm.amdgcn.fcmp, predicate OLT = 4), no
+      // bool round trip through a VGPR
+      const uint64_t mk = __builtin_amdgcn_fcmpf(dv, tau[r], 4) & live_mask;
+      const bool pass = (mk >> lane) & 1;
       if (mk) {
         const uint32_t hm = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
         if (pass) {
