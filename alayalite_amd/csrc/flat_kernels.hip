@@ -1,4 +1,4 @@
-// Flat (brute-force) exact k-NN on gfx950: the f32-MFMA contraction -2 Q B^T + |b|^2 with a fused
+// Flat (brute-force) exact k-NN on gfx950: the MFMA contraction -2 Q B^T + |b|^2 with a fused
 // per-query shortlist, then an exact rescoring pass.  The reference has no FLAT index
 // (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); its brute-force analogues are
 // find_exact_gt (include/utils/evaluate.hpp:29-62) and calc_gt (python/src/alayalite/utils.py:99-105).
@@ -10,14 +10,16 @@
 // flat_scan_kernel: 256 threads = 4 waves, 128 queries per block (32 per wave), one base chunk per
 // block.  Each wave holds its 32 queries as MFMA A fragments in VGPRs: lane l owns query (l & 31),
 // k in [h*K/2, (h+1)*K/2) with h = l >> 5 (the k order is free -- the GEMM only ranks candidates).
-// Base rows stream through a double-buffered LDS tile of 32 rows (row pitch K+4 floats, so the 16
-// lanes of a ds_read_b128 group hit distinct bank quads).  Per 32-row tile a wave issues K/2
-// v_mfma_f32_32x32x2f32 into one 32x32 accumulator (C[query][row]: row = lane & 31, query =
+// Base rows stream through a double-buffered LDS tile of 32 rows.  Default contraction: each f32 is
+// split into bf16 hi + lo when the tile is staged, and a 32-row tile costs 3 K/16
+// v_mfma_f32_32x32x16_bf16 (qh.bh + qh.bl + ql.bh); the f32 form (ALAYA_FLAT_F32) issues K/2
+// v_mfma_f32_32x32x2f32.  Both fill one 32x32 accumulator (C[query][row]: row = lane & 31, query =
 // (r&3) + 8(r>>2) + 4h for accumulator register r).  Approximate distance a = |b|^2 - 2 C.
-// Candidates below the query's running threshold are appended to a per-query LDS buffer.  The
-// shortlists themselves live in registers laid out like the accumulator (register r, half h <->
-// query (r&3) + 8(r>>2) + 4h, entry = lane & 31), so a buffer is folded in by a 32-lane bitonic
-// sort + merge on ds_swizzle, without leaving the half-wave that owns the query.
+// Candidates below the query's running threshold are appended to a per-query LDS buffer (a stack).
+// The shortlists themselves live in registers laid out like the accumulator (register r, half h
+// <-> query (r&3) + 8(r>>2) + 4h, entry = lane & 31), so 32 buffered candidates at a time are
+// folded in by a 32-lane bitonic sort + merge on DPP / ds_swizzle lane exchanges, without leaving
+// the half-wave that owns the query.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
