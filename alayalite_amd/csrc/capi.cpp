@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -128,6 +129,13 @@ struct alaya_index {
   std::unique_ptr<alaya_amd::RowMirror> upd_rows;
   std::unique_ptr<alaya_amd::UpdateContext> upd_ctx;
   hipStream_t stream = nullptr;
+  // Per-index scratch (work counter, visited spill area, flat candidates, SQ8 id buffer) is shared
+  // by every launch; `scratch_ev` marks the end of the last launch that used it, on
+  // `scratch_stream`.  A launch on another stream waits for it first (scratch_acquire), and calls
+  // that replace or free device buffers drain it (scratch_drain).
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_stream = nullptr;
+  bool scratch_used = false;
   uint64_t device_bytes() const {
     return base.bytes + valid.bytes + l0.bytes + levels.bytes + upper_off.bytes +
            upper_edges.bytes + eps.bytes + overflow.bytes + codes.bytes + sq_min.bytes + sq_max.bytes;
@@ -137,6 +145,22 @@ struct alaya_index {
 namespace {
 
 void set_device(const alaya_index *ix) { hip_check(hipSetDevice(ix->device), "hipSetDevice"); }
+
+// Order this call's launches on `s` after every earlier launch that used the index's scratch.
+void scratch_acquire(alaya_index *ix, hipStream_t s) {
+  if (ix->scratch_used && ix->scratch_stream != s)
+    hip_check(hipStreamWaitEvent(s, ix->scratch_ev, 0), "hipStreamWaitEvent");
+}
+// Mark the end of this call's launches on `s`.
+void scratch_release(alaya_index *ix, hipStream_t s) {
+  hip_check(hipEventRecord(ix->scratch_ev, s), "hipEventRecord");
+  ix->scratch_stream = s;
+  ix->scratch_used = true;
+}
+// Wait (host side) until no launch can still read or write the index's device buffers.
+void scratch_drain(alaya_index *ix) {
+  if (ix->scratch_used) hip_check(hipEventSynchronize(ix->scratch_ev), "hipEventSynchronize");
+}
 
 SearchParams base_params(alaya_index *ix) {
   SearchParams p{};
@@ -256,8 +280,10 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   ix->work.reserve(4);
   p.overflow_bits = ix->overflow.as<uint32_t>();
   p.work_counter = ix->work.as<uint32_t>();
+  scratch_acquire(ix, stream);
   hip_check(hipMemsetAsync(p.work_counter, 0, 4, stream), "hipMemsetAsync");
   hip_check(alaya_amd::launch_search(p, grid, lds, stream), "search launch");
+  scratch_release(ix, stream);
 }
 
 void ensure_norms(alaya_index *ix, hipStream_t stream) {
@@ -323,6 +349,7 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
   p.dim = ix->dim;
   p.stride = ix->stride;
   p.norms = ix->norms.as<float>();
+  p.valid = ix->has_valid ? ix->valid.as<uint32_t>() : nullptr;
   p.max_norm = ix->max_norm;
   // bf16 split contraction unless the rows are large enough for bf16(x) to overflow, or
   // ALAYA_FLAT_F32 is set (the f32-MFMA contraction; both feed the same exact rescoring)
@@ -383,10 +410,11 @@ int alaya_graph_load(const char *path, int id_bytes, alaya_graph **out) {
   });
 }
 
-int alaya_graph_save(const alaya_graph *g, const char *path, int id_bytes, uint64_t capacity) {
+int alaya_graph_save(const alaya_graph *g, const char *path, int id_bytes, uint64_t capacity,
+                     const uint8_t *valid_bitmap) {
   return guarded([&] {
     if (!g || !path) throw ArgError("invalid arguments");
-    alaya_amd::save_graph(g->g, path, id_bytes, capacity);
+    alaya_amd::save_graph(g->g, path, id_bytes, capacity, valid_bitmap);
   });
 }
 
@@ -469,6 +497,7 @@ int alaya_index_create(int device, alaya_index **out) {
     hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
     ix->num_cus = prop.multiProcessorCount;
     hip_check(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipEventCreateWithFlags(&ix->scratch_ev, hipEventDisableTiming), "hipEventCreate");
     *out = ix.release();
   });
 }
@@ -476,6 +505,8 @@ int alaya_index_create(int device, alaya_index **out) {
 void alaya_index_destroy(alaya_index *ix) {
   if (!ix) return;
   (void)hipSetDevice(ix->device);
+  if (ix->scratch_used) (void)hipEventSynchronize(ix->scratch_ev);
+  if (ix->scratch_ev) (void)hipEventDestroy(ix->scratch_ev);
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
   delete ix;
 }
@@ -487,7 +518,14 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     if (metric < ALAYA_METRIC_L2 || metric > ALAYA_METRIC_COS) throw ArgError("unknown metric");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
+    scratch_drain(ix);
     const uint32_t stride = round_up32(dim);
+    if (ix->has_sq8 && (n != ix->n || dim != ix->dim)) {  // the codes no longer describe these rows
+      ix->has_sq8 = false;
+      ix->codes.release();
+      ix->sq_min.release();
+      ix->sq_max.release();
+    }
     ix->base.release();
     ix->base.reserve(std::max<uint64_t>(n, 1) * stride * 4);
     if (n) {
@@ -530,6 +568,7 @@ int alaya_index_set_graph(alaya_index *ix, const alaya_graph *g) {
     if (h.has_overlay && (h.upper_R == 0 || h.upper_R > 64)) throw ArgError("overlay degree must be 1..64");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
+    scratch_drain(ix);
     auto up = [&](DevBuf &b, const void *src, size_t bytes) {
       b.release();
       b.reserve(std::max<size_t>(bytes, 4));
@@ -655,6 +694,7 @@ int alaya_index_reserve(alaya_index *ix, uint64_t capacity) {
     if (!ix) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
+    scratch_drain(ix);
     reserve_locked(ix, capacity);
   });
 }
@@ -694,6 +734,7 @@ int alaya_index_enable_updates(alaya_index *ix, const alaya_graph *g, const floa
     set_device(ix);
     if (g->g.n != n || ix->n != n || ix->graph_n != n) throw ArgError("graph, rows and device index sizes differ");
     if (capacity < n) throw ArgError("capacity below the stored rows");
+    scratch_drain(ix);
     auto m = std::make_unique<alaya_amd::RowMirror>();
     m->dim = ix->dim;
     m->metric = ix->metric;
@@ -872,6 +913,7 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
     if (R < 2 || R > 64 || R % 2) throw ArgError("max_nbrs must be even and in 2..64 for the device build");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
+    scratch_drain(ix);
     if (!ix->base.ptr || ix->n == 0) throw ArgError("index has no base vectors");
     if (ix->n >= (1ull << 31)) throw ArgError("ids must stay below 2^31 (LinearPool checked bit)");
     const uint64_t n = ix->n;
@@ -1061,6 +1103,18 @@ int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uin
   });
 }
 
+int alaya_index_shard_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
+                                    uint32_t ef, uint32_t *d_ids, float *d_dists, uint32_t *d_counters,
+                                    void *stream) {
+  return guarded([&] {
+    if (!ix || (nq && (!d_queries || !d_ids || !d_dists))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    do_search(ix, d_queries, nq, k, ef, d_ids, d_dists, d_counters, static_cast<hipStream_t>(stream), nullptr,
+              false, 0xffffffffu);
+  });
+}
+
 int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
                              uint32_t ef, uint32_t *ids, float *dists, uint32_t *counters) {
   return guarded([&] {
@@ -1190,6 +1244,7 @@ int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint3
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
     if (ix->base.ptr && (dim != ix->dim || n != ix->n)) throw ArgError("SQ8 codes do not match the base rows");
+    scratch_drain(ix);
     const uint32_t cs = (dim + 63) / 64 * 64;
     ix->codes.release();
     ix->codes.reserve(std::max<uint64_t>(n, 1) * cs);
@@ -1233,6 +1288,7 @@ static void sq8_search_dev(alaya_index *ix, const float *d_q, const float *d_rq,
   p.q_stride = ix->dim;
   alaya_amd::RerankParams r{ix->sq_ids.as<uint32_t>(), k, ef, ks, rerank == 2 ? 1 : 0, d_ids, d_dists};
   hip_check(alaya_amd::launch_rerank(p, r, s), "rerank launch");
+  scratch_release(ix, s);  // the rerank read the search's ids from the index's sq_ids buffer
 }
 
 int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
@@ -1285,6 +1341,7 @@ int alaya_index_flat_diag(alaya_index *ix, const float *d_queries, uint64_t nq, 
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    scratch_acquire(ix, s);
     ensure_norms(ix, s);
     int blocks = 0;
     alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
@@ -1292,6 +1349,7 @@ int alaya_index_flat_diag(alaya_index *ix, const float *d_queries, uint64_t nq, 
     p.ablate = ablate;
     p.merge_count = d_merge_count;
     hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
+    scratch_release(ix, s);
   });
 }
 
@@ -1303,12 +1361,14 @@ int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint
     set_device(ix);
     if (nq == 0) return;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    scratch_acquire(ix, s);
     ensure_norms(ix, s);
     int blocks = 0;
     alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
     flat_prescan(ix, p, &blocks, s);
     hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
     hip_check(alaya_amd::launch_flat_merge(p, s), "flat merge");
+    scratch_release(ix, s);
   });
 }
 
@@ -1320,6 +1380,7 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
     set_device(ix);
     if (n_recomputed) *n_recomputed = 0;
     if (nq == 0) return;
+    scratch_acquire(ix, ix->stream);
     ensure_norms(ix, ix->stream);
     ix->q_buf.reserve(nq * ix->dim * 4);
     ix->id_buf.reserve(nq * k * 4);
@@ -1332,14 +1393,17 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
     flat_prescan(ix, p, &blocks, ix->stream);
     hip_check(alaya_amd::launch_flat_scan(p, blocks, ix->stream), "flat scan");
     hip_check(alaya_amd::launch_flat_merge(p, ix->stream), "flat merge");
+    scratch_release(ix, ix->stream);
     std::vector<uint32_t> flags(nq);
     hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     std::vector<float> dv(nq * k);
     hip_check(hipMemcpyAsync(dv.data(), ix->dist_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     hip_check(hipMemcpyAsync(flags.data(), ix->flag_buf.ptr, nq * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     hip_check(hipStreamSynchronize(ix->stream), "flat search");
-    // queries whose shortlist bound did not hold: exhaustive exact distances on the device
+    // queries whose shortlist bound did not hold: exhaustive exact distances on the device, over
+    // the valid rows only (the scan never returns a row cleared in the validity bitmap)
     uint32_t redo = 0;
+    std::vector<uint32_t> vbits;
     for (uint64_t q = 0; q < nq; ++q) {
       if (!flags[q]) continue;
       ++redo;
@@ -1348,6 +1412,10 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
         for (uint64_t i = 0; i < ix->n; ++i) io[i] = static_cast<uint32_t>(i);
         ix->iota.reserve(ix->n * 4);
         hip_check(hipMemcpy(ix->iota.ptr, io.data(), ix->n * 4, hipMemcpyHostToDevice), "H2D");
+      }
+      if (ix->has_valid && vbits.empty()) {
+        vbits.assign((ix->n + 31) / 32, 0u);
+        hip_check(hipMemcpy(vbits.data(), ix->valid.ptr, vbits.size() * 4, hipMemcpyDeviceToHost), "D2H");
       }
       ix->dout_buf.reserve(ix->n * 4);
       SearchParams sp = base_params(ix);
@@ -1358,15 +1426,17 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
       std::vector<float> all(ix->n);
       hip_check(hipMemcpyAsync(all.data(), ix->dout_buf.ptr, ix->n * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
       hip_check(hipStreamSynchronize(ix->stream), "exhaustive");
-      std::vector<uint32_t> order(ix->n);
-      for (uint64_t i = 0; i < ix->n; ++i) order[i] = static_cast<uint32_t>(i);
-      const uint64_t kk = std::min<uint64_t>(k, ix->n);
+      std::vector<uint32_t> order;
+      order.reserve(ix->n);
+      for (uint64_t i = 0; i < ix->n; ++i)
+        if (vbits.empty() || ((vbits[i >> 5] >> (i & 31)) & 1u)) order.push_back(static_cast<uint32_t>(i));
+      const uint64_t kk = std::min<uint64_t>(k, order.size());
       std::partial_sort(order.begin(), order.begin() + kk, order.end(), [&](uint32_t a, uint32_t b) {
         return all[a] < all[b] || (all[a] == all[b] && a < b);
       });
-      for (uint64_t j = 0; j < k; ++j) {
-        ids[q * k + j] = j < kk ? order[j] : 0u;
-        dv[q * k + j] = j < kk ? all[order[j]] : 0.f;
+      for (uint64_t j = 0; j < k; ++j) {  // slots past the valid rows: (0xffffffff, FLT_MAX), as the scan
+        ids[q * k + j] = j < kk ? order[j] : 0xffffffffu;
+        dv[q * k + j] = j < kk ? all[order[j]] : FLT_MAX;
       }
     }
     if (dists) std::memcpy(dists, dv.data(), nq * k * 4);

@@ -13,6 +13,8 @@ struct FlatParams {
   uint32_t dim;
   uint32_t stride;     // multiple of 32, at most 256 for the MFMA scan
   const float *norms;  // |b|^2 per row
+  const uint32_t *valid;  // validity bitmap (bit i of word i/32), nullable = all rows valid;
+                          // removed / invalid rows are never returned
   float max_norm;      // max |b|
   const float *queries;
   uint64_t nq;

@@ -292,7 +292,8 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     }
     const float bn = nrm[buf * kTile + col];
     const uint32_t rid = static_cast<uint32_t>((row0 + col) * p.row_step);
-    const bool live = row0 + col < r1;
+    bool live = row0 + col < r1;
+    if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
     const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
     if (p.ablate == 1) {  // diagnostics: keep the accumulator live, skip the candidate path
       float sink = 0.f;
@@ -524,7 +525,8 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
     for (int f = 0; f < kL; ++f) {
       const float df = __shfl(dv, f);
       const uint32_t tf = __shfl(iv, f);
-      rank += before(df, tf, dv, iv) ? 1u : 0u;
+      // equal (distance, id) pairs (only the empty entries of a short list) rank by lane
+      rank += (before(df, tf, dv, iv) || (df == dv && tf == iv && f < lane)) ? 1u : 0u;
     }
     if (lane < kL && rank < p.k) {
       p.out_ids[qi * p.k + rank] = iv;

@@ -329,7 +329,8 @@ T get(std::ifstream &r) {
 }
 }  // namespace
 
-void save_graph(const HostGraph &g, const std::string &path, int id_bytes, uint64_t capacity) {
+void save_graph(const HostGraph &g, const std::string &path, int id_bytes, uint64_t capacity,
+                const uint8_t *valid) {
   if (id_bytes != 4 && id_bytes != 8) throw std::runtime_error("id_bytes must be 4 or 8");
   capacity = std::max<uint64_t>(capacity, g.n);
   std::ofstream w(path, std::ios::binary);
@@ -369,19 +370,32 @@ void save_graph(const HostGraph &g, const std::string &path, int id_bytes, uint6
     }
     w.write(row.data(), aligned);
   }
+  // Graph::insert sets a node's bit, Graph::remove (GraphUpdateJob::remove,
+  // graph_update_job.hpp:91-103 -> sequential_storage.hpp:94-100) clears it again.
   std::vector<uint8_t> bitmap((capacity + 7) / 8, 0);
-  for (uint64_t i = 0; i < g.n; ++i) bitmap[i / 8] |= static_cast<uint8_t>(1u << (i % 8));
+  for (uint64_t i = 0; i < g.n; ++i)
+    if (valid == nullptr || ((valid[i / 8] >> (i % 8)) & 1)) bitmap[i / 8] |= static_cast<uint8_t>(1u << (i % 8));
   w.write(reinterpret_cast<const char *>(bitmap.data()), bitmap.size());
   if (g.has_overlay) {  // overlay_graph.hpp:183-194
+    // node_num_ and ep_ are IDType but written with 4 bytes (the low half on little-endian hosts);
+    // each node's list is levels * max_nbrs IDType entries written with `cur * 4` bytes, so for
+    // 64-bit ids only the first cur / 2 entries reach the file (the reference's own width quirk).
     put<uint32_t>(w, static_cast<uint32_t>(capacity));
     put<uint32_t>(w, g.upper_R);
     put<uint32_t>(w, g.ep);
+    std::vector<uint64_t> wide;
     for (uint64_t i = 0; i < capacity; ++i) {
       const uint32_t lvl = i < g.n ? g.levels[i] : 0;
-      put<int32_t>(w, static_cast<int32_t>(lvl * g.upper_R));
-      if (lvl) {
-        w.write(reinterpret_cast<const char *>(&g.upper_edges[g.upper_off[i]]),
-                static_cast<std::streamsize>(lvl) * g.upper_R * 4);
+      const uint64_t cur = static_cast<uint64_t>(lvl) * g.upper_R;
+      put<int32_t>(w, static_cast<int32_t>(cur));
+      if (!cur) continue;
+      const uint32_t *src = &g.upper_edges[g.upper_off[i]];
+      if (id_bytes == 4) {
+        w.write(reinterpret_cast<const char *>(src), static_cast<std::streamsize>(cur) * 4);
+      } else {
+        wide.assign(cur, 0);
+        for (uint64_t j = 0; j < cur; ++j) wide[j] = src[j] == 0xffffffffu ? ~0ull : src[j];
+        w.write(reinterpret_cast<const char *>(wide.data()), static_cast<std::streamsize>(cur) * 4);
       }
     }
   }
@@ -442,8 +456,17 @@ HostGraph load_graph(const std::string &path, int id_bytes) {
     for (uint32_t i = 0; i < node_num; ++i) {
       const int32_t cur = get<int32_t>(r);
       if (cur < 0) throw std::runtime_error("corrupt overlay");
-      std::vector<uint32_t> buf(cur);
-      if (cur) r.read(reinterpret_cast<char *>(buf.data()), static_cast<std::streamsize>(cur) * 4);
+      // OverlayGraph::load reads cur * 4 bytes into a list of cur IDType entries pre-filled with -1
+      // (overlay_graph.hpp:151-170): for 64-bit ids the first cur / 2 entries, the rest stay -1
+      std::vector<uint32_t> buf(cur, 0xffffffffu);
+      if (cur && id_bytes == 4) {
+        r.read(reinterpret_cast<char *>(buf.data()), static_cast<std::streamsize>(cur) * 4);
+      } else if (cur) {
+        std::vector<uint64_t> wide(cur, ~0ull);
+        r.read(reinterpret_cast<char *>(wide.data()), static_cast<std::streamsize>(cur) * 4);
+        for (int32_t j = 0; j < cur; ++j) buf[j] = wide[j] == ~0ull ? 0xffffffffu : static_cast<uint32_t>(wide[j]);
+      }
+      if (!r) throw std::runtime_error("truncated overlay");
       if (i < g.n) {
         g.levels[i] = static_cast<uint32_t>(cur) / g.upper_R;
         g.upper_off[i] = g.upper_edges.size();

@@ -44,7 +44,9 @@ std::vector<uint32_t> hnsw_levels(uint64_t n, uint32_t M, uint64_t seed);
 
 // Reference on-disk format (graph.hpp:165-238 + overlay_graph.hpp:151-194 +
 // sequential_storage.hpp:110-142), IDType = uint32 or uint64 (id_bytes 4 or 8).
-void save_graph(const HostGraph &g, const std::string &path, int id_bytes, uint64_t capacity);
+// valid: the graph storage bitmap (bit i%8 of byte i/8; NULL = every stored node valid)
+void save_graph(const HostGraph &g, const std::string &path, int id_bytes, uint64_t capacity,
+                const uint8_t *valid = nullptr);
 HostGraph load_graph(const std::string &path, int id_bytes);
 
 }  // namespace alaya_amd

@@ -244,7 +244,8 @@ class PyIndexInterface {
   void save(const std::string &index_path, const std::string &data_path, const std::string &quant_path) {
     if (!graph_) throw std::runtime_error("index is not fitted");
     sync_graph();
-    check(alaya_graph_save(graph_, index_path.c_str(), id_bytes_, std::max<uint64_t>(params_.capacity_, n_)));
+    check(alaya_graph_save(graph_, index_path.c_str(), id_bytes_, std::max<uint64_t>(params_.capacity_, n_),
+                           valid_.empty() ? nullptr : valid_.data()));
     if (!data_path.empty()) save_raw(data_path);
     if (!quant_path.empty()) {
       if (params_.quantization_type_ != QuantizationType::SQ8) throw std::runtime_error("no quantized space to save");
@@ -669,7 +670,7 @@ class Graph {
     return std::make_shared<Graph>(g);
   }
   void save(const std::string &path, int id_bytes, uint64_t capacity) const {
-    check(alaya_graph_save(g_, path.c_str(), id_bytes, capacity));
+    check(alaya_graph_save(g_, path.c_str(), id_bytes, capacity, nullptr));
   }
   py::tuple arrays() const {
     uint64_t n, nue;
@@ -754,6 +755,12 @@ class DeviceIndex {
   void search_device(uintptr_t q, uint64_t nq, uint32_t k, uint32_t ef, uintptr_t ids, uintptr_t dists,
                      uintptr_t counters, uintptr_t stream) {
     check(alaya_index_batch_search_device(ix_, reinterpret_cast<const float *>(q), nq, k, ef,
+                                          reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
+                                          reinterpret_cast<uint32_t *>(counters), reinterpret_cast<void *>(stream)));
+  }
+  void shard_search_device(uintptr_t q, uint64_t nq, uint32_t k, uint32_t ef, uintptr_t ids, uintptr_t dists,
+                           uintptr_t counters, uintptr_t stream) {
+    check(alaya_index_shard_search_device(ix_, reinterpret_cast<const float *>(q), nq, k, ef,
                                           reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
                                           reinterpret_cast<uint32_t *>(counters), reinterpret_cast<void *>(stream)));
   }
@@ -936,6 +943,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
            py::arg("seed") = 100, py::arg("batch_div") = 0, py::arg("max_batch") = 0, py::arg("refine") = 2)
       .def("search", &DeviceIndex::search, py::arg("queries"), py::arg("k"), py::arg("ef"))
       .def("search_device", &DeviceIndex::search_device)
+      .def("shard_search_device", &DeviceIndex::shard_search_device)
       .def("distances", &DeviceIndex::distances)
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
       .def("set_visited_mode", &DeviceIndex::set_visited_mode)

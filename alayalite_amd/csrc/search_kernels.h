@@ -37,7 +37,8 @@ struct SearchParams {
   uint32_t *out_ids;      // nq x k
   float *out_dists;       // nq x k (nullable)
   uint32_t *out_counters; // nq x 4 (n_dist, n_expand, n_dist_upper, n_hops_upper), nullable
-  uint32_t fill_id;       // id written for result slots past the pool (0 = reference behaviour)
+  uint32_t fill_id;       // id written for result slots past the pool (0 = reference behaviour, with
+                          // distance 0.0; 0xffffffff = empty slot, with distance FLT_MAX)
   // scratch
   uint32_t *work_counter; // zeroed before each launch
   uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area

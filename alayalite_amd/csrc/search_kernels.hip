@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     // ---- results (ids[i] = pool.id(i), distances[i] = pool.dist(i)) --------------------------
     for (uint32_t i = lane; i < p.k; i += 64) {
       uint32_t id = p.fill_id;
-      float d = 0.f;
+      float d = p.fill_id == kEmpty ? FLT_MAX : 0.f;  // kEmpty fill (shard / corrected rerank) sorts last
       if (i < ps.size) {
         id = L.pi[i] & kIdMask;
         d = L.pd[i];

@@ -46,16 +46,28 @@ def unpack_candidates(packed):
     return gid, bits.view(torch.float32)
 
 
+EMPTY = 0xFFFFFFFF  # an empty result slot of a shard search (shard_search_device): (EMPTY, FLT_MAX)
+
+
+def to_global(local_ids, offset: int):
+    """Shard-local ids -> global ids; empty slots (0xffffffff) stay empty."""
+    import torch
+
+    ids = local_ids.to(torch.int64) & 0xFFFFFFFF
+    return torch.where(ids == EMPTY, ids, ids + offset)
+
+
 def exchange_and_merge(local_ids, local_dists, offset: int, k: int, group=None):
     """local_ids: [nq, k] shard-local ids (int32/int64 tensor); returns merged global (ids, dists).
     One all_gather of packed (distance, id) keys and one sort: the smallest k keys are the top-k
-    by (distance, global id)."""
+    by (distance, global id).  Empty slots (id 0xffffffff, distance FLT_MAX) sort after every real
+    candidate and appear in the result only when all shards together hold fewer than k."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     device = local_ids.device
-    packed = pack_candidates(local_ids.to(torch.int64) + offset, local_dists)
+    packed = pack_candidates(to_global(local_ids, offset), local_dists)
     if dist.get_backend(group) == "gloo" and device.type != "cpu":  # gloo gathers host tensors
         packed = packed.cpu()
     parts = [torch.empty_like(packed) for _ in range(world)]
@@ -70,8 +82,12 @@ def merge_reference(ids_per_shard, dists_per_shard, offsets, k):
     nq = ids_per_shard[0].shape[0]
     out_i = np.zeros((nq, k), np.int64)
     out_d = np.zeros((nq, k), np.float32)
+    def glob(a, off):
+        a = a.astype(np.int64) & 0xFFFFFFFF
+        return np.where(a == EMPTY, a, a + off)
+
     for q in range(nq):
-        ids = np.concatenate([ids_per_shard[s][q].astype(np.int64) + offsets[s] for s in range(len(offsets))])
+        ids = np.concatenate([glob(ids_per_shard[s][q], offsets[s]) for s in range(len(offsets))])
         ds = np.concatenate([dists_per_shard[s][q] for s in range(len(offsets))])
         o = np.lexsort((ids, ds))[:k]
         out_i[q], out_d[q] = ids[o], ds[o]
@@ -93,8 +109,9 @@ class ShardedIndex:
         self.index.set_graph(self.graph)
 
     def search_device(self, q_dev, k: int, ef: int, ids_dev, dists_dev, counters_dev, stream):
-        self.index.search_device(q_dev.data_ptr(), q_dev.shape[0], k, ef, ids_dev.data_ptr(),
-                                 dists_dev.data_ptr(), counters_dev.data_ptr(), stream)
+        """This shard's search; result slots past the pool are (0xffffffff, FLT_MAX)."""
+        self.index.shard_search_device(q_dev.data_ptr(), q_dev.shape[0], k, ef, ids_dev.data_ptr(),
+                                       dists_dev.data_ptr(), counters_dev.data_ptr(), stream)
 
     def search(self, q_dev, k: int, ef: int, stream, group=None):
         import torch

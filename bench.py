@@ -5,7 +5,9 @@ ef reaching recall@10 >= 0.95 against exact ground truth, bracketed by the refer
 {10,20,40,60,80,120,200,400,600,800} and narrowed by bisection to ~1%.  The CPU baseline runs at
 the same ef.  Inputs (rows, graph, queries) are resident in HBM before the timed region.
 
-N > 1 (torchrun, one rank per GPU):
+N > 1 (one rank per GPU): under torchrun (WORLD_SIZE set, it must equal --gpus), or started as
+`python bench.py --gpus N`, which launches the N ranks itself (127.0.0.1 rendezvous) before any GPU
+call; rank 0 prints the JSON line.  The workload is config 4 (10k queries) unless --nq says otherwise.
   --mode shard   (default) base rows partitioned by range, one HNSW graph per shard, every rank
                  searches all queries on its shard, per-shard top-k exchanged with an RCCL
                  all_gather over xGMI and merged by (distance, global id).  Total work fixed:
@@ -79,8 +81,9 @@ def parse():
                    help="N>1 shard mode: skip the replica-mode leg reported beside the shard result")
     p.add_argument("--build-threads", type=int, default=0)
     p.add_argument("--builder", choices=("auto", "host", "gpu"), default="auto",
-                   help="graph builder: host = HNSWBuilder restated on the host (cached), gpu = the "
-                        "device batched build (alaya_index_build_graph); auto = gpu from 2M rows up")
+                   help="graph builder: host = HNSWBuilder restated on the host (cached; multi-threaded, so "
+                        "not deterministic), gpu = the device batched build (alaya_index_build_graph, "
+                        "deterministic); auto = gpu")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cache-dir", default=os.path.join(ROOT, "data_cache"))
@@ -91,9 +94,11 @@ def parse():
     p.add_argument("--sweep-qps", action="store_true",
                    help="also time every ef of the sweep (config 3 reports the whole QPS/recall curve)")
     a = p.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.workload in WORKLOADS:
         w = WORKLOADS[a.workload]
-        a.nq = a.nq or w["nq"]
+        # N > 1 GIST: config 4 (10k queries sharded over the GPUs); N = 1: the metric's 1k queries
+        a.nq = a.nq or (10_000 if (world > 1 and a.workload == "gist-hnsw") else w["nq"])
         a.dim = a.dim or w["dim"]
         a.n = a.n or w.get("n", 1_000_000)
     else:
@@ -103,11 +108,76 @@ def parse():
     return a
 
 
-def host_threads():
+def _affinity():
     try:
-        return max(1, min(16, len(os.sched_getaffinity(0))))
+        return max(1, len(os.sched_getaffinity(0)))
     except AttributeError:  # pragma: no cover
-        return max(1, min(16, os.cpu_count() or 1))
+        return max(1, os.cpu_count() or 1)
+
+
+def _cgroup_cpus():
+    """CPU quota of this process's cgroup (cgroup v2 cpu.max / v1 cfs quota), or None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return float(quota) / float(period)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            quota = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            period = float(f.read())
+        if quota > 0:
+            return quota / period
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_threads():
+    """Every core this process may run on -- the affinity set, capped by the cgroup's CPU quota when
+    there is one (a quota of 16 CPUs on a 192-thread host runs 16 threads' worth, more threads only
+    add contention).  The CPU baseline uses all of them."""
+    q = _cgroup_cpus()
+    return max(1, min(_affinity(), int(q + 0.999))) if q else _affinity()
+
+
+def host_info():
+    """nproc, the affinity size and the CPU model of this host (recorded with the CPU baseline)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    q = _cgroup_cpus()
+    return {"nproc": os.cpu_count(), "affinity": _affinity(), "cgroup_cpus": None if q is None else round(q, 2),
+            "threads_used": host_threads(), "cpu_model": model}
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without torchrun: start N ranks of this script (RANK/LOCAL_RANK/WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1) as child processes -- before this process touches the GPU -- and return
+    the worst exit code.  Rank 0's stdout carries the JSON line."""
+    import socket
+    import subprocess
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
 
 
 def graph_for(native, base, efc, threads, cache_dir, tag, metric=0):
@@ -283,7 +353,8 @@ def run_flat(args):
         same = int(sum(set(cpu_ids[i].tolist()) == set(got[i].tolist()) for i in range(m)))
         cpu = {"value": round(m / sec, 1), "unit": "queries/s", "cores": ct, "kind": "port",
                "sample": f"{m} of {nq} queries, find_exact_gt restated (l2_sqr AVX2 order + std::sort per query), "
-                         f"queries over {ct} threads; top-{K} sets equal to the device's on {same}/{m}"}
+                         f"queries over {ct} threads; top-{K} sets equal to the device's on {same}/{m}",
+               "host": host_info()}
         log("cpu baseline", cpu)
     out = {
         "metric": "QPS, flat exact k-NN, 1M x 128 L2, 1k queries (BASELINE config 2)",
@@ -313,6 +384,13 @@ def run_flat(args):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"[bench] WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}: refusing to report "
+                  f"a different GPU count", file=sys.stderr, flush=True)
+            return 2
+    elif args.gpus > 1:
+        return spawn_ranks(args.gpus)
     if args.workload == "flat":
         return run_flat(args)
     import torch
@@ -356,7 +434,7 @@ def main():
         lo, hi = 0, args.n
         my_base = base
         tag = f"{w['gen']}_m{metric}" if w["gen"] != "gist_like" else "gist"
-    builder = args.builder if args.builder != "auto" else ("gpu" if my_base.shape[0] >= 2_000_000 else "host")
+    builder = args.builder if args.builder != "auto" else "gpu"
     index = native.DeviceIndex(local)
     index.set_base(my_base, metric)
     if builder == "gpu":
@@ -389,6 +467,10 @@ def main():
         if use_sq8:  # SQ8 graph search + PyIndex::rerank as batch_search runs it (rerank mode 1)
             ix.search_sq8_device(q_dev.data_ptr(), 0, nq, K, ef, 1, ids_dev.data_ptr(), dists_dev.data_ptr(),
                                  cnt_dev.data_ptr(), stream.cuda_stream)
+        elif world > 1 and args.mode == "shard" and ix is index:
+            # per-shard search: slots past the pool are (0xffffffff, FLT_MAX), never a spurious hit
+            ix.shard_search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
+                                   cnt_dev.data_ptr(), stream.cuda_stream)
         else:
             ix.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
                              cnt_dev.data_ptr(), stream.cuda_stream)
@@ -467,6 +549,32 @@ def main():
     # ---- timed region ------------------------------------------------------------------------
     elapsed, kernel_ms = timed(ef, args.steps, args.warmup)
 
+    # ---- PCIe-inclusive rate (reported beside value, never value): the host-buffer API's work --
+    # queries H2D from pinned host memory, the search, ids + distances D2H, each step synchronised
+    pcie = None
+    if world == 1:
+        q_host = torch.from_numpy(queries).pin_memory()
+        ids_host = torch.empty((nq, K), dtype=torch.int32).pin_memory()
+        d_host = torch.empty((nq, K), dtype=torch.float32).pin_memory()
+
+        def host_step():
+            q_dev.copy_(q_host, non_blocking=True)
+            launch(ef)
+            ids_host.copy_(ids_dev, non_blocking=True)
+            d_host.copy_(dists_dev, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+
+        for _ in range(max(1, args.warmup)):
+            host_step()
+        t_p = time.perf_counter()
+        for _ in range(args.steps):
+            host_step()
+        el_p = time.perf_counter() - t_p
+        pcie = {"value": round(nq * args.steps / el_p, 1), "unit": "queries/s",
+                "ms_per_step": round(el_p / args.steps * 1e3, 4),
+                "note": "H2D queries (pinned) + search + D2H ids and distances, synchronised per step"}
+        log("pcie-inclusive", pcie)
+
     # ---- algorithmic bytes from the kernel's counters -------------------------
     cnt = cnt_dev.cpu().numpy().astype(np.int64)
     row_bytes = args.dim if use_sq8 else 4 * args.dim  # SQ8 codes are 1 B per dimension
@@ -539,6 +647,8 @@ def main():
             out["config"]["qps_curve"] = curve
         if replica is not None:
             out["replica"] = replica
+        if pcie is not None:
+            out["pcie_inclusive"] = pcie
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -631,8 +741,9 @@ def cpu_baseline(args, graph, base, queries, ef, metric, sq8, device_ids):
     return {"value": round(m / med, 1), "unit": "queries/s", "cores": ct, "kind": "port",
             "sample": f"{m} of {nq} queries at ef={ef} ({what}), median of {len(runs)} runs after 1 warm-up "
                       f"(Scheduler begin->join{' + rerank loop' if sq8 is not None else ''}), "
-                      f"ids_equal_to_device={parity}"}
+                      f"ids_equal_to_device={parity}",
+            "host": host_info()}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -6,6 +6,13 @@
  * the last failure on the calling thread.  Host buffers are copied; *_device variants take device
  * pointers and a hipStream_t (passed as void*) and are asynchronous on that stream.
  *
+ * Streams: an index keeps per-index scratch (work counter, visited-set spill area, flat and SQ8
+ * candidate buffers).  Every launching call orders itself after the previous launching call on the
+ * index (a hipStreamWaitEvent when the streams differ), so calls on different streams serialise on
+ * the device instead of racing; calls that replace device buffers (set_base, set_graph, set_sq8,
+ * build_graph, reserve, enable_updates, destroy) first wait for those launches to finish.  Calls on
+ * one index from several host threads are serialised by the index's lock.
+ *
  * Reference interfaces each group replaces (paths relative to the AlayaLite repo root):
  *   alaya_index_*            PyIndex<HNSWBuilder<RawSpace>, Space> state and lifetime
  *                            (python/include/index.hpp:85-506, PyIndexInterface :508-587)
@@ -57,7 +64,10 @@ int alaya_graph_build_hnsw(const float *data, uint64_t n, uint32_t dim, int metr
                            uint32_t ef_construction, uint32_t num_threads, uint64_t seed,
                            alaya_graph **out);
 int alaya_graph_load(const char *path, int id_bytes, alaya_graph **out);
-int alaya_graph_save(const alaya_graph *g, const char *path, int id_bytes, uint64_t capacity);
+/* valid_bitmap (nullable): the graph storage bitmap, ceil(n/8) bytes; a node removed with
+ * GraphUpdateJob::remove has its bit cleared in the reference's file (sequential_storage.hpp:94-100). */
+int alaya_graph_save(const alaya_graph *g, const char *path, int id_bytes, uint64_t capacity,
+                     const uint8_t *valid_bitmap);
 /* sizes: n, R, has_overlay, upper_R, ep, max_level, n_upper_edges, n_eps */
 int alaya_graph_info(const alaya_graph *g, uint64_t *n, uint32_t *R, int *has_overlay,
                      uint32_t *upper_R, uint32_t *ep, uint32_t *max_level,
@@ -88,6 +98,13 @@ int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq,
 int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uint64_t nq,
                                     uint32_t k, uint32_t ef, uint32_t *d_ids, float *d_dists,
                                     uint32_t *d_counters, void *stream);
+/* The per-shard search of a base-range sharded index (no reference counterpart): as
+ * alaya_index_batch_search_device, except that result slots past the pool (shard rows < k, or
+ * ef < k) hold (0xffffffff, FLT_MAX) instead of the reference's (0, 0.0), so they sort after every
+ * real candidate in the cross-shard merge.  d_dists is required. */
+int alaya_index_shard_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
+                                    uint32_t ef, uint32_t *d_ids, float *d_dists, uint32_t *d_counters,
+                                    void *stream);
 /* ---- device graph construction (Index.fit on the MI355X) ------------------------------------
  * Replaces HNSWBuilder::build_graph (include/index/graph/hnsw/hnsw_builder.hpp:98-194) over hnswlib
  * add_point (include/index/graph/hnsw/hnswlib.hpp:652-751), from the index's own rows

@@ -28,7 +28,18 @@ def _shard_results(rank, nq=37, k=10, n_per=500, seed=0):
     return ids, d
 
 
-def _worker(rank, world, port, out_path):
+def _with_empty_slots(rank, ids, d):
+    """A shard search with fewer pool entries than k (shard rows < k or ef < k) fills the rest with
+    (0xffffffff, FLT_MAX) (alaya_index_shard_search_device)."""
+    if rank == 1:
+        ids, d = ids.copy(), d.copy()
+        ids[:, 4:] = -1  # int32 view of 0xffffffff
+        d[:, 4:] = np.finfo(np.float32).max
+        d[:3, :4] = 0.0  # shard 1's real candidates precede shard 0's for the first queries
+    return ids, d
+
+
+def _worker(rank, world, port, out_path, empty=False):
     import torch.distributed as dist
 
     from alayalite_amd.sharded import exchange_and_merge
@@ -36,6 +47,8 @@ def _worker(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ids, d = _shard_results(rank)
+    if empty:
+        ids, d = _with_empty_slots(rank, ids, d)
     mi, md = exchange_and_merge(torch.from_numpy(ids), torch.from_numpy(d), rank * 500, 10)
     if rank == 0:
         np.savez(out_path, ids=mi.numpy(), d=md.numpy())
@@ -64,6 +77,32 @@ def test_exchange_and_merge_gloo(tmp_path):
     ref_i, ref_d = merge_reference([p[0] for p in parts], [p[1] for p in parts], [0, 500], 10)
     assert np.array_equal(got["ids"], ref_i)
     assert np.array_equal(got["d"], ref_d)
+
+
+def test_exchange_with_empty_slots_gloo(tmp_path):
+    """Empty slots never displace a real candidate (a (0, 0.0) fill became a spurious top
+    hit); with fewer than k real candidates in all shards together the result ends in empty slots."""
+    import torch.multiprocessing as mp
+
+    from alayalite_amd.sharded import EMPTY, merge_reference
+
+    out = str(tmp_path / "merged.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out, True), nprocs=2, join=True)
+    got = np.load(out)
+    parts = [_with_empty_slots(r, *_shard_results(r)) for r in range(2)]
+    ref_i, ref_d = merge_reference([p[0] for p in parts], [p[1] for p in parts], [0, 500], 10)
+    assert np.array_equal(got["ids"], ref_i) and np.array_equal(got["d"], ref_d)
+    assert not (got["ids"] == EMPTY).any()  # shard 0 alone holds 10 real candidates per query
+    assert (got["ids"][:3, :4] >= 500).all()  # shard 1's zero-distance rows come first
+    # fewer than k real candidates overall: the merged tail is empty slots
+    from alayalite_amd.sharded import pack_candidates, to_global, unpack_candidates
+
+    a_i, a_d = np.full((2, 3), -1, np.int32), np.full((2, 3), np.finfo(np.float32).max, np.float32)
+    a_i[:, 0], a_d[:, 0] = 7, 1.5
+    keys = torch.cat([pack_candidates(to_global(torch.from_numpy(a_i), 0), torch.from_numpy(a_d)),
+                      pack_candidates(to_global(torch.from_numpy(a_i), 100), torch.from_numpy(a_d))], 1)
+    gi, gd = unpack_candidates(torch.sort(keys, 1).values[:, :4])
+    assert gi[0].tolist() == [7, 107, EMPTY, EMPTY]
 
 
 def test_packed_keys_order_like_dist_then_id():
