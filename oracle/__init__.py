@@ -40,6 +40,7 @@ class OrcIndex(C.Structure):
         ("sq_min", C.c_void_p),
         ("sq_max", C.c_void_p),
         ("sq8_variant", C.c_int),
+        ("generic", C.c_int),
     ]
 
 
@@ -54,8 +55,8 @@ class OrcCounters(C.Structure):
 
 def build(force: bool = False) -> str:
     """Compile liboracle.so with the committed Makefile (gcc only, no GPU)."""
-    src = os.path.join(_HERE, "oracle.cpp")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("oracle.cpp", "oracle_build.cpp", "oracle.h", "Makefile")]
+    if force or not os.path.exists(_LIB_PATH) or any(os.path.getmtime(_LIB_PATH) < os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
@@ -117,6 +118,13 @@ def lib():
         for name in ("orc_sq8_l2", "orc_sq8_ip"):
             getattr(_lib, name).restype = f
             getattr(_lib, name).argtypes = [p, p, sz, p, p, C.c_int]
+        _lib.orc_hnsw_build.restype = p
+        _lib.orc_hnsw_build.argtypes = [p, C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                        C.c_uint64]
+        _lib.orc_hnsw_upper_slots.restype = C.c_uint64
+        _lib.orc_hnsw_upper_slots.argtypes = [p]
+        _lib.orc_hnsw_export.argtypes = [p, p, p, p, p, p]
+        _lib.orc_hnsw_free.argtypes = [p]
         _lib.orc_cpu_has_avx2_fma.restype = C.c_int
         _lib.orc_cpu_has_avx512f.restype = C.c_int
     return _lib
@@ -195,8 +203,10 @@ class IndexView:
     """Host arrays of one index (base rows + HNSW graph) in the layout orc_index expects."""
 
     def __init__(self, base, l0, levels, upper_off, upper_edges, upper_R, ep, metric=L2, valid=None,
-                 sq8=None):
-        """sq8 = (codes[n, d] uint8, min[d], max[d], variant) switches the search space to SQ8Space."""
+                 sq8=None, generic=False):
+        """sq8 = (codes[n, d] uint8, min[d], max[d], variant) switches the search space to SQ8Space.
+        generic = True: the rows are a non-float DataType cast to float, compared with the generic
+        l2_sqr<T>/ip_sqr<T> branch (distance_l2.ipp:735-741) instead of the AVX2 float kernel."""
         self.base = np.ascontiguousarray(base, np.float32)
         self.l0 = np.ascontiguousarray(l0, np.uint32)
         self.levels = None if levels is None else np.ascontiguousarray(levels, np.uint32)
@@ -209,7 +219,7 @@ class IndexView:
             base=_ptr(self.base), n=self.base.shape[0], dim=self.base.shape[1], stride=self.base.shape[1],
             valid=_ptr(self.valid), metric=metric, l0=_ptr(self.l0), R=self.l0.shape[1],
             levels=_ptr(self.levels), upper_off=_ptr(self.upper_off), upper_edges=_ptr(self.upper_edges),
-            upper_R=upper_R, ep=ep)
+            upper_R=upper_R, ep=ep, generic=1 if generic else 0)
         if sq8 is not None:
             codes, mn, mx, variant = sq8
             self.codes = np.ascontiguousarray(codes, np.uint8)
@@ -300,6 +310,26 @@ class Updater:
         d = np.zeros(k, np.float32)
         lib().orc_search(lib().orc_updater_view(self._h), _ptr(q), k, ef, _ptr(ids), _ptr(d), None)
         return ids, d
+
+
+def build_hnsw(base, metric=L2, R=32, ef_construction=100, seed=100, generic=False):
+    """HNSWBuilder::build_graph with one thread, restated (oracle_build.cpp).  Returns the graph as
+    (l0[n, R], levels[n], upper_off[n], upper_edges, ep, upper_R) in the engine's Graph.arrays()
+    layout."""
+    b = np.ascontiguousarray(base, np.float32)
+    n, dim = b.shape
+    h = lib().orc_hnsw_build(_ptr(b), n, dim, metric, 1 if generic else 0, R, ef_construction, seed)
+    try:
+        slots = lib().orc_hnsw_upper_slots(h)
+        l0 = np.zeros((n, R), np.uint32)
+        levels = np.zeros(n, np.uint32)
+        off = np.zeros(n, np.uint64)
+        ue = np.zeros(max(slots, 1), np.uint32)
+        ep = np.zeros(1, np.uint32)
+        lib().orc_hnsw_export(h, _ptr(l0), _ptr(levels), _ptr(off), _ptr(ue), _ptr(ep))
+    finally:
+        lib().orc_hnsw_free(h)
+    return l0, levels, off, ue[:slots], int(ep[0]), R
 
 
 def sq8_fit(data):

@@ -225,7 +225,10 @@ struct QC {
       return sq8_dist_any(ix->metric, qcode.data(), ix->codes + static_cast<uint64_t>(u) * ix->code_stride,
                           ix->dim, ix->sq_min, ix->sq_max, ix->sq8_variant);
     if (ix->valid && !((ix->valid[u >> 3] >> (u & 7)) & 1)) return FLT_MAX;
-    return fast_dist(ix->metric, q, ix->base + static_cast<uint64_t>(u) * ix->stride, ix->dim);
+    const float *row = ix->base + static_cast<uint64_t>(u) * ix->stride;
+    if (ix->generic)
+      return ix->metric == ORC_L2 ? generic_l2(q, row, ix->dim) : generic_ip(q, row, ix->dim);
+    return fast_dist(ix->metric, q, row, ix->dim);
   }
 };
 
@@ -667,6 +670,7 @@ struct orc_updater {
     if (!((valid[u >> 3] >> (u & 7)) & 1)) return FLT_MAX;
     const float *x = base.data() + static_cast<size_t>(q) * view.dim;
     const float *y = base.data() + static_cast<size_t>(u) * view.dim;
+    if (view.generic) return view.metric == ORC_L2 ? generic_l2(x, y, view.dim) : generic_ip(x, y, view.dim);
     return view.metric == ORC_L2 ? orc_l2_f32(x, y, view.dim) : orc_ip_f32(x, y, view.dim);
   }
   void update(uint32_t node) {  // :105-137

@@ -22,6 +22,8 @@
  *   orc_updater_*                   GraphUpdateJob insert_and_update / update / remove
  *                                   (executor/jobs/graph_update_job.hpp:49-137) with JobContext
  *                                   (job_context.hpp:25-29), Graph/RawSpace insert + remove
+ *   orc_hnsw_*                      HNSWBuilder::build_graph, one thread (oracle_build.cpp:
+ *                                   hnsw_builder.hpp:98-194, hnswlib.hpp:87-751)
  *   orc_sq8_*                       SQ8Quantizer (space/quant/sq8.hpp:99-143) and the AVX-512 /
  *                                   AVX2 SQ8 kernels (distance_l2.ipp:244-408, distance_ip.ipp:198-366)
  *
@@ -85,6 +87,9 @@ typedef struct {
   uint32_t code_stride;
   const float *sq_min, *sq_max;
   int sq8_variant;            /* 0 generic, 1 AVX2, 2 AVX-512 (get_*_sq8_func host choice)       */
+  int generic;                /* 1: non-float DataType -- the rows (cast to float) are compared with
+                                 the generic branch of l2_sqr<T>/ip_sqr<T> (distance_l2.ipp:735-741,
+                                 distance_ip.ipp:744-750) instead of the AVX2 float kernel          */
 } orc_index;
 
 typedef struct {
@@ -125,6 +130,19 @@ void orc_updater_free(orc_updater *u);
 const orc_index *orc_updater_view(orc_updater *u);
 int64_t orc_updater_insert(orc_updater *u, const float *search_query, const float *row, uint32_t ef);
 void orc_updater_remove(orc_updater *u, uint32_t id);
+
+/* ---- HNSW construction (oracle_build.cpp) ------------------------------------------------------
+ * HNSWBuilder::build_graph with one thread (hnsw_builder.hpp:98-194 over hnswlib.hpp:87-751):
+ * M = R/2, M0 = R, ef = max(ef_construction, M), levels from default_random_engine(seed).
+ * export: l0[n*R] (-1 padded), levels[n], upper_off[n], upper_edges[upper_slots] (R per level,
+ * -1 padded), ep.  generic = 1: the non-float DataType distance branch. */
+typedef struct orc_hnsw orc_hnsw;
+orc_hnsw *orc_hnsw_build(const float *rows, uint64_t n, uint32_t dim, int metric, int generic, uint32_t R,
+                         uint32_t ef_construction, uint64_t seed);
+uint64_t orc_hnsw_upper_slots(const orc_hnsw *o);
+void orc_hnsw_export(const orc_hnsw *o, uint32_t *l0, uint32_t *levels, uint64_t *upper_off,
+                     uint32_t *upper_edges, uint32_t *ep);
+void orc_hnsw_free(orc_hnsw *o);
 
 /* ---- SQ8 ---------------------------------------------------------------------------------- */
 /* find_exact_gt (include/utils/evaluate.hpp:29-62): per query, l2_sqr to every row, std::sort of

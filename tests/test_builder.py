@@ -1,5 +1,10 @@
 """Host HNSW builder (product) + reference on-disk graph format; checked with the oracle search.
 
+Parity: with one thread the product builder (csrc/hnsw_build.cpp) must produce the reference's
+graph exactly -- the oracle's independent restatement of HNSWBuilder::build_graph (oracle_build.cpp,
+from hnswlib.hpp:87-751 and hnsw_builder.hpp:98-194), edge for edge, level for level, same entry
+point -- including data with massive distance ties (heap order) and degenerate sizes.
+
 Reference coverage restated: python/tests/test_index_types.py:32-80 (recall >= 0.9 on 1k x 128 for
 float32/int32/uint32/uint8 data), tests/index/graph_test.cpp:89-130 and hnsw_test.cpp:72-119
 (save/load round trip edge by edge)."""
@@ -37,6 +42,47 @@ def test_builder_structure(native, c1):
             lst = ue[off[u] + (lvl - 1) * 32: off[u] + lvl * 32]
             valid = lst[lst != 0xFFFFFFFF]
             assert len(valid) <= 16 and all(levels[v] >= lvl for v in valid)
+
+
+def _builder_case(name):
+    import zlib
+
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    metric, R, efc, seed = 0, 32, 100, 100
+    if name == "c1":
+        base = np.random.default_rng(0).random((1000, 128), dtype=np.float32)
+    elif name == "ip96":
+        base, metric = rng.standard_normal((800, 96)).astype(np.float32), 1
+    elif name == "cos100":
+        base = rng.standard_normal((600, 100)).astype(np.float32)
+        base /= np.linalg.norm(base, axis=1, keepdims=True)
+        metric = 2
+    elif name == "int_ties":  # many equal distances: the heaps' tie order decides the edges
+        base = rng.integers(0, 4, (1500, 32)).astype(np.float32)
+    elif name == "duplicates":
+        base = np.repeat(rng.random((200, 24), dtype=np.float32), 4, axis=0)
+    elif name == "R16_efc8_seed7":  # ef_construction < M -> ef = M (hnswlib.hpp:104)
+        base, R, efc, seed = rng.random((700, 40), dtype=np.float32), 16, 8, 7
+    elif name == "R64":
+        base, R = rng.random((900, 20), dtype=np.float32), 64
+    elif name == "gist_like":
+        c = rng.uniform(0, 0.5, (16, 960)).astype(np.float32)
+        base = np.clip(c[rng.integers(0, 16, 1200)] + rng.normal(0, 0.05, (1200, 960)), 0, 1).astype(np.float32)
+    else:  # tiny sizes
+        base = rng.random((int(name[1:]), 8), dtype=np.float32)
+    return base, metric, R, efc, seed
+
+
+@pytest.mark.parametrize("name", ["c1", "ip96", "cos100", "int_ties", "duplicates", "R16_efc8_seed7", "R64",
+                                  "gist_like", "n1", "n2", "n17", "n33"])
+def test_host_builder_equals_oracle_builder(native, orc, name):
+    base, metric, R, efc, seed = _builder_case(name)
+    l0, levels, off, ue, ep, upper_r, _ = native.Graph.build(base, metric, R, efc, 1, seed).arrays()
+    o_l0, o_levels, o_off, o_ue, o_ep, o_r = orc.build_hnsw(base, metric, R, efc, seed)
+    assert np.array_equal(l0, o_l0)
+    assert np.array_equal(levels, o_levels) and np.array_equal(off, o_off)
+    assert np.array_equal(ue, o_ue)
+    assert (ep, upper_r) == (o_ep, o_r)
 
 
 def test_single_thread_build_is_deterministic(native, c1):

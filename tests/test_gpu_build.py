@@ -124,20 +124,20 @@ def test_installed_graph_equals_host_copy_and_oracle(native, orc):
         assert tuple(cnt[i]) == tuple(r_c)
 
 
-def test_single_point_batches_reproduce_the_sequential_build(native):
+@pytest.mark.parametrize("dim,n", [(24, 1500), (960, 600)])
+def test_single_point_batches_reproduce_the_sequential_build(native, orc, dim, n):
     """batch_div = max_batch = 1, no refine: points are inserted one at a time in label order, which
     is the reference's sequential add_point (num_threads = 1).  On tie-free data the device graph
-    equals the host restatement's graph exactly (hnswlib.hpp:652-751)."""
-    base, _ = _data(1500, 1, 24, 17)
+    equals the oracle's restatement of HNSWBuilder::build_graph exactly (oracle_build.cpp from
+    hnswlib.hpp:652-751), and so the product's host build too."""
+    base, _ = _data(n, 1, dim, 17)
     for metric in (0, 1):
         _, g, st = _build(native, base, metric=metric, batch_div=1, max_batch=1, refine=0)
-        host = native.Graph.build(base, metric, 32, 100, 1, 100)
         assert st["max_batch"] == 1
-        for a, b in zip(g.arrays(), host.arrays()):
-            if isinstance(a, np.ndarray):
-                assert np.array_equal(a, b)
-            else:
-                assert a == b
+        l0, levels, off, ue, ep, upper_r, _ = g.arrays()
+        o_l0, o_levels, o_off, o_ue, o_ep, o_r = orc.build_hnsw(base, metric, 32, 100, 100)
+        assert np.array_equal(l0, o_l0) and np.array_equal(levels, o_levels)
+        assert np.array_equal(off, o_off) and np.array_equal(ue, o_ue) and (ep, upper_r) == (o_ep, o_r)
 
 
 @pytest.mark.parametrize("batch_div,max_batch", [(1, 1), (2, 64), (64, 0)])

@@ -1,9 +1,10 @@
 """Generate the committed golden fixtures under tests/golden/ (run from the repo root).
 
-Inputs are seeded synthetic data (BASELINE config 1 shapes); the graph is built by the engine's
-single-threaded HNSW builder (hnswlib order, seed 100); expected ids/distances come from the CPU
-restatement in oracle/ (the checker).  The reference itself cannot be built or run here
-(SURVEY.md §8c), so these vectors pin the restatement and the device path to each other; the
+Inputs are seeded synthetic data (BASELINE config 1 shapes); the graph is built by the oracle's
+restatement of HNSWBuilder::build_graph with one thread (oracle/oracle_build.cpp: hnswlib order,
+seed 100); expected ids/distances/counters come from the oracle's search restatement.  Nothing here
+runs the product (alayalite_amd), so the fixtures pin the engine's builders and its device search
+to the restatement.  The reference itself cannot be built or run here; the
 restatement is pinned to the reference by its own known-answer tests (tests/test_oracle.py).
 """
 
@@ -19,15 +20,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import oracle  # noqa: E402
-from alayalite_amd import _native  # noqa: E402
 
 EFS = (10, 20, 50, 100)
 
 
 def fixture(name, base, queries, metric, k=10):
-    ext = _native._ext
-    g = ext.Graph.build(base, metric, 32, 100, 1, 100)
-    l0, levels, off, ue, ep, upper_r, _ = g.arrays()
+    l0, levels, off, ue, ep, upper_r = oracle.build_hnsw(base, metric, 32, 100, 100)
     view = oracle.IndexView(base, l0, levels, off, ue, upper_r, ep, metric=metric)
     out = {"queries": queries, "l0": l0, "levels": levels, "upper_off": off, "upper_edges": ue,
            "ep": np.uint32(ep), "upper_R": np.uint32(upper_r), "metric": np.int32(metric),
