@@ -400,7 +400,7 @@ const void *sym(Which w, bool ip) {
 // apply kernels compare a row with <= 32 others per step and are latency-bound, so they take the
 // generic distance loop (~100 VGPRs instead of ~400) for more resident waves.
 const void *kernel_for(Which w, const SearchParams &p) {
-  const uint32_t chunks = (p.dim % 32 == 0) ? p.dim / 32 : 0;
+  const uint32_t chunks = (!p.generic && p.dim % 32 == 0) ? p.dim / 32 : 0;
 #define ALAYA_CASE(C) \
   if (chunks == C) return sym<C>(w, p.ip);
   ALAYA_BUILD_CHUNKS(ALAYA_CASE)

@@ -100,6 +100,7 @@ struct alaya_index {
   uint64_t n = 0;
   uint32_t dim = 0, stride = 0;
   int metric = ALAYA_METRIC_L2;
+  bool generic = false;  // ALAYA_DIST_GENERIC: non-float DataType rows, generic distance order
   DevBuf base, valid;
   bool has_valid = false;
   // graph
@@ -170,6 +171,7 @@ SearchParams base_params(alaya_index *ix) {
   p.stride = ix->stride;
   p.valid = ix->has_valid ? ix->valid.as<uint32_t>() : nullptr;
   p.ip = ix->metric != ALAYA_METRIC_L2;
+  p.generic = ix->generic;
   return p;
 }
 
@@ -341,6 +343,7 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
                                   float *d_dists, uint32_t *d_flags, int *blocks) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
   if (ix->metric != ALAYA_METRIC_L2) throw ArgError("the flat MFMA path supports the L2 metric");
+  if (ix->generic) throw ArgError("the flat MFMA path ranks float32 rows (not the generic non-float order)");
   if (alaya_amd::flat_scan_lds(ix->stride) == 0) throw ArgError("the flat MFMA path supports dim <= 224");
   if (k == 0 || k > static_cast<uint32_t>(alaya_amd::flat_shortlist()) - 8) throw ArgError("flat search needs 1 <= k <= 24");
   alaya_amd::FlatParams p{};
@@ -394,6 +397,8 @@ int alaya_graph_build_hnsw(const float *data, uint64_t n, uint32_t dim, int metr
                            alaya_graph **out) {
   return guarded([&] {
     if (!out || (n && !data) || dim == 0) throw ArgError("invalid arguments");
+    if ((metric & ~ALAYA_DIST_GENERIC) < ALAYA_METRIC_L2 || (metric & ~ALAYA_DIST_GENERIC) > ALAYA_METRIC_COS)
+      throw ArgError("unknown metric");
     if (n >= (1ull << 31)) throw ArgError("ids must stay below 2^31 (LinearPool checked bit)");
     auto g = std::make_unique<alaya_graph>();
     g->g = alaya_amd::build_hnsw(data, n, dim, metric, R, ef_construction, num_threads, seed);
@@ -515,6 +520,8 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
                          const uint8_t *valid_bitmap) {
   return guarded([&] {
     if (!ix || (n && !rows) || dim == 0) throw ArgError("invalid arguments");
+    const bool generic = (metric & ALAYA_DIST_GENERIC) != 0;
+    metric &= ~ALAYA_DIST_GENERIC;
     if (metric < ALAYA_METRIC_L2 || metric > ALAYA_METRIC_COS) throw ArgError("unknown metric");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -551,6 +558,7 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     ix->dim = dim;
     ix->stride = stride;
     ix->metric = metric;
+    ix->generic = generic;
     ix->overflow.release();
     ix->norms_ready = false;
     ix->capacity = n;
@@ -737,7 +745,7 @@ int alaya_index_enable_updates(alaya_index *ix, const alaya_graph *g, const floa
     scratch_drain(ix);
     auto m = std::make_unique<alaya_amd::RowMirror>();
     m->dim = ix->dim;
-    m->metric = ix->metric;
+    m->metric = ix->metric | (ix->generic ? ALAYA_DIST_GENERIC : 0);
     m->rows.assign(rows, rows + n * ix->dim);
     m->valid.assign((capacity + 7) / 8 + 1, 0);
     for (uint64_t i = 0; i < n; ++i) {

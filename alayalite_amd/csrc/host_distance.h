@@ -101,7 +101,29 @@ inline bool host_has_avx2() {
   return ok;
 }
 
+// Generic branch of l2_sqr<T> / ip_sqr<T> for non-float DataType (distance_l2.ipp:735-741,
+// distance_ip.ipp:744-750), the same order as the device's generic_distances: one float
+// accumulator, elements in order, no contraction (the library is built -ffp-contract=off).
+template <bool kInner>
+inline float dist_generic(const float *x, const float *y, size_t dim) {
+  float sum = 0.0f;
+  for (size_t i = 0; i < dim; ++i) {
+    if (kInner) {
+      sum += x[i] * y[i];
+    } else {
+      const float d = x[i] - y[i];
+      sum += d * d;
+    }
+  }
+  return kInner ? -sum : sum;
+}
+
+// flag OR-ed into a metric code: the rows are a non-float DataType (ALAYA_DIST_GENERIC,
+// include/alaya_hip.h)
+constexpr int kDistGeneric = 0x100;
+
 inline float host_dist(int metric, const float *x, const float *y, size_t dim) {
+  if (metric & kDistGeneric) return (metric & 0xff) == kL2 ? dist_generic<false>(x, y, dim) : dist_generic<true>(x, y, dim);
   if (host_has_avx2()) return metric == kL2 ? dist_avx2<false>(x, y, dim) : dist_avx2<true>(x, y, dim);
   return metric == kL2 ? dist_portable<false>(x, y, dim) : dist_portable<true>(x, y, dim);
 }

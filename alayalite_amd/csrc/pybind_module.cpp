@@ -104,6 +104,11 @@ class PyIndexInterface {
     if (params_.metric_ == MetricType::COS && dtype_ != kF32 && dtype_ != kF64) {
       throw std::runtime_error("COS metric only support float or double");  // raw_space.hpp:88-93
     }
+    // SQ8 over a non-float DataType takes the reference's generic SQ8 branch (distance_l2.ipp:750-763,
+    // quantize in double arithmetic for double data, sq8.hpp:118-130), which the device does not
+    // implement: refuse rather than return different neighbours.
+    if (params_.quantization_type_ == QuantizationType::SQ8 && dtype_ != kF32)
+      throw std::runtime_error("SQ8 quantization of non-float32 data is not supported by the MI355X engine");
     check(alaya_index_create(0, &ix_));
   }
   ~PyIndexInterface() {
@@ -142,7 +147,7 @@ class PyIndexInterface {
     if (builder == "gpu") {
       {
         py::gil_scoped_release nogil;
-        check(alaya_index_set_base(ix_, rows_f32_.data(), n, dim_, metric_code(), nullptr));
+        check(alaya_index_set_base(ix_, rows_f32_.data(), n, dim_, dist_code(), nullptr));
         check(alaya_index_build_graph(ix_, params_.max_nbrs_, ef_construction, 100, 0, 0, 2, &graph_, nullptr));
       }
       if (params_.quantization_type_ == QuantizationType::SQ8) {
@@ -155,7 +160,7 @@ class PyIndexInterface {
     }
     {
       py::gil_scoped_release nogil;
-      check(alaya_graph_build_hnsw(rows_f32_.data(), n, dim_, metric_code(), params_.max_nbrs_,
+      check(alaya_graph_build_hnsw(rows_f32_.data(), n, dim_, dist_code(), params_.max_nbrs_,
                                    ef_construction, num_threads, 100, &graph_));
     }
     if (params_.quantization_type_ == QuantizationType::SQ8) train_sq8(num_threads);
@@ -321,6 +326,10 @@ class PyIndexInterface {
     }
   }
 
+  // the metric plus ALAYA_DIST_GENERIC for non-float DataType: l2_sqr<T>/ip_sqr<T> take their generic
+  // branch for every DataType but float (distance_l2.ipp:735-741, distance_ip.ipp:744-750)
+  int dist_code() const { return metric_code() | (dtype_ != kF32 ? ALAYA_DIST_GENERIC : 0); }
+
   void check_dtype(const py::array &a) const {
     if (dtype_code(a.dtype()) != dtype_) throw std::runtime_error("Unsupported data type");
   }
@@ -418,7 +427,7 @@ class PyIndexInterface {
     uint64_t gn = 0;
     check(alaya_graph_info(graph_, &gn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
     py::gil_scoped_release nogil;
-    check(alaya_index_set_base(ix_, rows_f32_.data(), n_, dim_, metric_code(),
+    check(alaya_index_set_base(ix_, rows_f32_.data(), n_, dim_, dist_code(),
                                valid_.empty() ? nullptr : valid_.data()));
     check(alaya_index_set_graph(ix_, graph_));
     if (!sq_codes_.empty())

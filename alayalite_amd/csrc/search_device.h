@@ -203,9 +203,46 @@ __device__ __forceinline__ void finish_rows(const SearchParams &p, const float *
   }
 }
 
+// The generic branch of l2_sqr<T> / ip_sqr<T> for non-float DataType (distance_l2.ipp:735-741,
+// distance_ip.ipp:744-750): elements cast to float, one accumulator over the elements in order,
+// diff*diff (x*y) rounded before the add (-ffp-contract=off).  The reference builds it with -Ofast,
+// which leaves the order to the compiler; the source order is the restatement's (oracle generic_l2),
+// and every order agrees while the partial sums stay integers below 2^24.  One lane per row.
+template <bool kIP>
+__device__ __forceinline__ void generic_distances(const SearchParams &p, const float *q,
+                                                  const uint32_t *ids, int n, float *out) {
+  const int lane = lane_id();
+  for (int base = 0; base < n; base += 64) {
+    const int r = base + lane;
+    if (r < n) {
+      const uint32_t id = ids[r];
+      const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
+      float sum = 0.f;
+      for (uint32_t e = 0; e < p.dim; ++e) {
+        if (kIP) {
+          sum += q[e] * row[e];
+        } else {
+          const float d = q[e] - row[e];
+          sum += d * d;
+        }
+      }
+      float res = kIP ? -sum : sum;
+      if (p.valid != nullptr && !((p.valid[id >> 5] >> (id & 31)) & 1u)) res = FLT_MAX;
+      out[r] = res;
+    }
+  }
+  wave_sync();
+}
+
 template <bool kIP, int kChunks>
 __device__ __forceinline__ void row_distances(const SearchParams &p, const float *q,
                                               const uint32_t *ids, int n, float *out) {
+  if constexpr (kChunks == 0) {
+    if (p.generic) {  // wave-uniform; the host selects the kChunks == 0 kernels for generic rows
+      generic_distances<kIP>(p, q, ids, n, out);
+      return;
+    }
+  }
   const int lane = lane_id();
   const int g = lane >> 3, m = lane & 7;
   const int T = kChunks > 0 ? kChunks : static_cast<int>(p.dim >> 5);

@@ -16,6 +16,8 @@ struct SearchParams {
   uint32_t stride;        // multiple of 32 floats (128 B rows, 16 B aligned float4 loads)
   const uint32_t *valid;  // SequentialStorage validity bitmap as 32-bit words; nullptr = all valid
   bool ip;                // IP / COS (negated inner product) vs L2
+  bool generic;           // non-float DataType: generic l2_sqr<T>/ip_sqr<T> order (one accumulator,
+                          // elements in order; distance_l2.ipp:735-741), not the AVX2 float order
   // level-0 adjacency (Graph), n x R, -1 padded
   const uint32_t *l0;
   uint32_t R;

@@ -400,10 +400,10 @@ static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped) {
   return ip ? kernel_ptr<true, 0, false, kSpace>() : kernel_ptr<false, 0, false, kSpace>();
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order) {
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic) {
   if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped);
   if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped);
-  const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
+  const uint32_t chunks = (!generic && dim % 32 == 0) ? dim / 32 : 0;  // generic order: the runtime-d kernel
   if (stamped) {
     if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();
     if (chunks == 4) return ip ? kernel_ptr<true, 4, true>() : kernel_ptr<false, 4, true>();
@@ -422,7 +422,7 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_or
 }
 
 hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, lds, stream);
@@ -441,7 +441,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 }
 
 hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, lds);
 }
 

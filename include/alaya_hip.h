@@ -50,6 +50,11 @@ extern "C" {
 #define ALAYA_METRIC_L2 0
 #define ALAYA_METRIC_IP 1
 #define ALAYA_METRIC_COS 2
+/* OR-ed into the metric of alaya_index_set_base / alaya_graph_build_hnsw: the rows are a non-float
+ * DataType (int8, uint8, int32, uint32, double) cast to float, and distances follow the generic
+ * branch of l2_sqr<T> / ip_sqr<T> (include/simd/distance_l2.ipp:735-741, distance_ip.ipp:744-750:
+ * one float accumulator over the elements in order) instead of the AVX2 float kernel. */
+#define ALAYA_DIST_GENERIC 0x100
 
 typedef struct alaya_index alaya_index;
 typedef struct alaya_graph alaya_graph;

@@ -85,6 +85,26 @@ def test_host_builder_equals_oracle_builder(native, orc, name):
     assert (ep, upper_r) == (o_ep, o_r)
 
 
+@pytest.mark.parametrize("kind", ["float64", "int32_wide"])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_host_builder_generic_order_equals_oracle(native, orc, kind, metric):
+    """Non-float DataType (A10): RawSpace<T>::get_distance takes the generic l2_sqr<T>/ip_sqr<T>
+    branch (distance_l2.ipp:735-741), so the builder compares rows in that order (metric |
+    ALAYA_DIST_GENERIC).  Data whose partial sums are not exact in float, so the order matters."""
+    rng = np.random.default_rng(60 + metric)
+    if kind == "float64":
+        data = rng.standard_normal((700, 50))
+    else:
+        data = rng.integers(-3000, 3000, (700, 40)).astype(np.int32)
+    rows = data.astype(np.float32)
+    gen = [orc.lib().orc_l2_generic(orc._ptr(rows[0]), orc._ptr(rows[i]), rows.shape[1], 0) for i in range(1, 40)]
+    assert any(np.float32(a) != orc.l2(rows[0], rows[i + 1]) for i, a in enumerate(gen))  # the order is visible
+    l0, levels, off, ue, ep, upper_r, _ = native.Graph.build(rows, metric | 0x100, 32, 100, 1, 100).arrays()
+    o_l0, o_levels, o_off, o_ue, o_ep, o_r = orc.build_hnsw(rows, metric, 32, 100, 100, generic=True)
+    assert np.array_equal(l0, o_l0) and np.array_equal(levels, o_levels)
+    assert np.array_equal(ue, o_ue) and (ep, upper_r) == (o_ep, o_r)
+
+
 def test_single_thread_build_is_deterministic(native, c1):
     base, _ = c1
     a = native.Graph.build(base, 0, 32, 100, 1, 100).arrays()

@@ -236,6 +236,41 @@ def test_index_save_load(native, c1, tmp_path):
     assert again.get_dim() == 128
 
 
+def _typed_data(dtype, n, nq, d, seed):
+    rng = np.random.default_rng(seed)
+    if dtype == np.float64:
+        return rng.standard_normal((n, d)), rng.standard_normal((nq, d))
+    lo, hi = {np.int8: (-100, 100), np.uint8: (0, 256), np.int32: (-5000, 5000), np.uint32: (0, 9000)}[dtype]
+    return rng.integers(lo, hi, (n, d)).astype(dtype), rng.integers(lo, hi, (nq, d)).astype(dtype)
+
+
+@pytest.mark.parametrize("dtype", [np.int8, np.uint8, np.int32, np.uint32, np.float64])
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+def test_non_float_dtypes_bit_exact(native, orc, dtype, metric):
+    """A10: Index.fit / batch_search on int8, uint8, int32, uint32 and float64 rows.  The reference's
+    RawSpace<T> compares them with the generic branch of l2_sqr<T>/ip_sqr<T> (distance_l2.ipp:735-741,
+    distance_ip.ipp:744-750): elements cast to float, one accumulator in order.  The int32/uint32
+    and float64 data have partial sums that are not exact in float, so the order is visible.  Graph
+    = the oracle's builder (generic order); search ids and distance bits = the oracle's search."""
+    import alayalite_amd
+
+    base, queries = _typed_data(dtype, 2500, 24, 48, 70 + (metric == "ip"))
+    index = alayalite_amd.Client().create_index(f"t_{np.dtype(dtype).name}_{metric}", capacity=2500, data_type=dtype,
+                                                metric=metric)
+    index.fit(base, ef_construction=100, num_threads=1)
+    ids, dists = index.batch_search_with_distance(queries, 10, 64)
+    l0, levels, off, ue, ep, upper_r, _ = index.native().graph_arrays()
+    rows, qf = base.astype(np.float32), queries.astype(np.float32)
+    m = 0 if metric == "l2" else 1
+    o_l0, o_levels, o_off, o_ue, o_ep, _ = orc.build_hnsw(rows, m, 32, 100, 100, generic=True)
+    assert np.array_equal(l0, o_l0) and np.array_equal(ue, o_ue) and ep == o_ep
+    view = orc.IndexView(rows, l0, levels, off, ue, upper_r, ep, metric=m, generic=True)
+    for i in range(len(qf)):
+        r_ids, r_d = view.search(qf[i], 10, 64)
+        assert np.array_equal(ids[i].astype(np.uint32), r_ids), i
+        assert np.array_equal(dists[i].view(np.uint32), r_d.view(np.uint32)), i
+
+
 def test_uint64_ids_and_int_dtype(native, c1):
     import alayalite_amd
 
