@@ -141,6 +141,149 @@ __device__ __forceinline__ void fold32(float &L, uint32_t &Li, float cd, uint32_
   fold32_sorted(L, Li, cd, ci, col);
 }
 
+// Shortlists of one wave (32 queries) in registers with the accumulator's layout: register r of
+// half h holds the ascending list of query (r & 3) + 8 (r >> 2) + 4h, entry (lane & 31).  cnt[r] =
+// buffered candidates of that query (uniform over the half), tau[r] = its current 32nd distance;
+// full / nonempty: registers whose buffer holds >= kTile / > 0 candidates (uniform).
+struct Shortlists {
+  float ld[16], tau[16];
+  uint32_t li[16];
+  int cnt[16];
+  uint32_t full, nonempty;
+};
+
+__device__ __forceinline__ void init_shortlists(const FlatParams &p, uint64_t q0, int h, Shortlists &S) {
+  S.full = S.nonempty = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    S.ld[r] = FLT_MAX;
+    S.li[r] = 0xffffffffu;
+    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    S.tau[r] = (p.tau_init && qi < p.nq) ? p.tau_init[qi] : FLT_MAX;
+    S.cnt[r] = 0;
+  }
+}
+
+// write the per-(chunk, query) shortlist
+__device__ __forceinline__ void store_shortlists(const FlatParams &p, uint64_t q0, int chunk, const Shortlists &S) {
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (qi < p.nq) {
+      const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
+      p.cand_d[o] = S.ld[r];
+      p.cand_i[o] = S.li[r];
+    }
+  }
+}
+
+// Candidate handling of one 32-row tile: approximate distances a = |b|^2 - 2 c[r] below the
+// query's threshold are appended to its LDS buffer (bd/bi, a stack per query), then the fold
+// rounds that became due run.  last: the wave's final tile (every buffer is drained).
+__device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x16 &c, float bn, uint32_t rid,
+                                                uint64_t live_mask, bool last, Shortlists &S, float *bd,
+                                                uint32_t *bi, uint64_t &t_app, uint64_t &t_fold) {
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  // append candidates below each query's threshold (counts stay in registers).  The common case
+  // per register is fma, compare, one uniform branch: the bookkeeping for folds (`S.full`,
+  // `S.nonempty`, `need`) changes only when a register takes an append, so it lives inside that
+  // branch, in scalar masks carried across tiles.
+  const uint64_t ta = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
+  uint32_t need = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
+    const float dv = fmaf(-2.0f, c[r], bn);
+    // the compare's lane mask straight from v_cmp (llvm.amdgcn.fcmp, predicate OLT = 4), no
+    // bool round trip through a VGPR
+    const uint64_t mk = __builtin_amdgcn_fcmpf(dv, S.tau[r], 4) & live_mask;
+    const bool pass = (mk >> lane) & 1;
+    if (mk) {
+      const uint32_t hm = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
+      if (pass) {
+        const int pos = S.cnt[r] + __popc(hm & ((1u << col) - 1u));
+        bd[qloc * kBuf + pos] = dv;
+        bi[qloc * kBuf + pos] = rid;
+      }
+      S.cnt[r] += __popc(hm);
+      S.nonempty |= 1u << r;
+      if (__builtin_amdgcn_ballot_w64(S.cnt[r] >= kTile)) {
+        S.full |= 1u << r;
+        if (__builtin_amdgcn_ballot_w64(S.cnt[r] > kBuf - kTile)) need |= 1u << r;  // could overflow next tile
+      }
+    }
+  }
+  // A fold round takes the newest 32 entries of a buffer (it is a stack), so a round costs the
+  // same wherever it happens.  Due rounds: buffers that could overflow on the next tile (one round
+  // brings > 64 down to <= 64).  Smoothing: otherwise one round of a buffer holding a S.full batch.
+  // At most ~one round per wave per tile keeps the four waves level between barriers.  The last
+  // tile drains every buffer.
+  if (last) need |= S.nonempty;
+  if (need == 0 && S.full) need = 1u << __builtin_ctz(S.full);
+  if (p.ablate == 2) {  // diagnostics: appends only, buffers dropped instead of folded
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (need & (1u << r)) S.cnt[r] = 0;
+    S.full &= ~need;
+    S.nonempty &= ~need;
+    need = 0;
+  }
+  // Fold rounds for the registers in `need`.  One copy of the
+  // fold body (a uniform loop over `need`, the register picked by value): unrolling it per
+  // register would put ~48 KB of code in the loop and thrash the instruction cache.
+  const uint64_t tf = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
+  t_app += tf - ta;
+  if (need) {
+    wave_fence();
+    do {
+      const int r = __builtin_ctz(need);
+      need &= need - 1;
+      float L = S.ld[0];
+      uint32_t Li = S.li[0];
+      int cr = S.cnt[0];
+#pragma unroll
+      for (int r2 = 1; r2 < 16; ++r2) {
+        if (r2 == r) {
+          L = S.ld[r2];
+          Li = S.li[r2];
+          cr = S.cnt[r2];
+        }
+      }
+      const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;
+      do {  // one round; the last tile repeats until the buffer is empty
+        const int start = max(cr - 32, 0);  // uniform per half
+        float cd = FLT_MAX;
+        uint32_t ci = 0xffffffffu;
+        if (start + col < cr) {
+          cd = bd[qloc * kBuf + start + col];
+          ci = bi[qloc * kBuf + start + col];
+        }
+        fold32(L, Li, cd, ci, col);
+        cr = start;
+      } while (last && __builtin_amdgcn_ballot_w64(cr > 0));
+      if (__builtin_amdgcn_ballot_w64(cr >= kTile)) S.full |= 1u << r;
+      else S.full &= ~(1u << r);
+      if (!__builtin_amdgcn_ballot_w64(cr > 0)) S.nonempty &= ~(1u << r);
+      const float th = lane31_of_half(L);
+#pragma unroll
+      for (int r2 = 0; r2 < 16; ++r2) {
+        if (r2 == r) {
+          S.ld[r2] = L;
+          S.li[r2] = Li;
+          S.cnt[r2] = cr;
+          S.tau[r2] = th;
+        }
+      }
+      if (lane == 0 && p.merge_count) atomicAdd(p.merge_count + blockIdx.x, 1u);
+    } while (need);
+    wave_fence();
+  }
+  t_fold += (p.merge_count ? __builtin_amdgcn_s_memtime() : 0) - tf;
+}
+
 template <int K, bool kSplit>
 __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   static_assert(K % 16 == 0 && K <= 256, "K must be a multiple of 16, at most 256");
@@ -195,21 +338,8 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
         al[s][j] = lo;
       }
   }
-  // Shortlists live in registers with the accumulator's layout: register r of half h holds the
-  // ascending list of query qloc(r, h), entry (lane & 31).  cnt[r] = buffered candidates of that
-  // query (uniform over the half), tau[r] = its current 32nd distance.
-  float ld[16], tau[16];
-  uint32_t li[16];
-  int cnt[16];
-  uint32_t full = 0, nonempty = 0;  // registers whose buffer holds >= kTile / > 0 candidates (uniform)
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    ld[r] = FLT_MAX;
-    li[r] = 0xffffffffu;
-    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    tau[r] = (p.tau_init && qi < p.nq) ? p.tau_init[qi] : FLT_MAX;
-    cnt[r] = 0;
-  }
+  Shortlists S;
+  init_shortlists(p, q0, h, S);
 
   // cooperative tile load: 32 rows x K floats, 256 threads, float4 each
   constexpr int kVecPerRow = K / 4;
@@ -307,102 +437,8 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
       __syncthreads();
       continue;
     }
-    // append candidates below each query's threshold (counts stay in registers).  The common case
-    // per register is fma, compare, one uniform branch: the bookkeeping for folds (`full`,
-    // `nonempty`, `need`) changes only when a register takes an append, so it lives inside that
-    // branch, in scalar masks carried across tiles.
-    const uint64_t ta = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
-    uint32_t need = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
-      const float dv = fmaf(-2.0f, c[r], bn);
-      // the compare's lane mask straight from v_cmp (llvm.amdgcn.fcmp, predicate OLT = 4), no
-      // bool round trip through a VGPR
-      const uint64_t mk = __builtin_amdgcn_fcmpf(dv, tau[r], 4) & live_mask;
-      const bool pass = (mk >> lane) & 1;
-      if (mk) {
-        const uint32_t hm = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
-        if (pass) {
-          const int pos = cnt[r] + __popc(hm & ((1u << col) - 1u));
-          bd[qloc * kBuf + pos] = dv;
-          bi[qloc * kBuf + pos] = rid;
-        }
-        cnt[r] += __popc(hm);
-        nonempty |= 1u << r;
-        if (__builtin_amdgcn_ballot_w64(cnt[r] >= kTile)) {
-          full |= 1u << r;
-          if (__builtin_amdgcn_ballot_w64(cnt[r] > kBuf - kTile)) need |= 1u << r;  // could overflow next tile
-        }
-      }
-    }
-    // A fold round takes the newest 32 entries of a buffer (it is a stack), so a round costs the
-    // same wherever it happens.  Due rounds: buffers that could overflow on the next tile (one round
-    // brings > 64 down to <= 64).  Smoothing: otherwise one round of a buffer holding a full batch.
-    // At most ~one round per wave per tile keeps the four waves level between barriers.  The last
-    // tile drains every buffer.
-    if (!more) need |= nonempty;
-    if (need == 0 && full) need = 1u << __builtin_ctz(full);
-    if (p.ablate == 2) {  // diagnostics: appends only, buffers dropped instead of folded
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (need & (1u << r)) cnt[r] = 0;
-      full &= ~need;
-      nonempty &= ~need;
-      need = 0;
-    }
-    // Fold rounds for the registers in `need`.  One copy of the
-    // fold body (a uniform loop over `need`, the register picked by value): unrolling it per
-    // register would put ~48 KB of code in the loop and thrash the instruction cache.
-    const uint64_t tf = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
-    t_app += tf - ta;
-    if (need) {
-      wave_fence();
-      do {
-        const int r = __builtin_ctz(need);
-        need &= need - 1;
-        float L = ld[0];
-        uint32_t Li = li[0];
-        int cr = cnt[0];
-#pragma unroll
-        for (int r2 = 1; r2 < 16; ++r2) {
-          if (r2 == r) {
-            L = ld[r2];
-            Li = li[r2];
-            cr = cnt[r2];
-          }
-        }
-        const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;
-        do {  // one round; the last tile repeats until the buffer is empty
-          const int start = max(cr - 32, 0);  // uniform per half
-          float cd = FLT_MAX;
-          uint32_t ci = 0xffffffffu;
-          if (start + col < cr) {
-            cd = bd[qloc * kBuf + start + col];
-            ci = bi[qloc * kBuf + start + col];
-          }
-          fold32(L, Li, cd, ci, col);
-          cr = start;
-        } while (!more && __builtin_amdgcn_ballot_w64(cr > 0));
-        if (__builtin_amdgcn_ballot_w64(cr >= kTile)) full |= 1u << r;
-        else full &= ~(1u << r);
-        if (!__builtin_amdgcn_ballot_w64(cr > 0)) nonempty &= ~(1u << r);
-        const float th = lane31_of_half(L);
-#pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) {
-          if (r2 == r) {
-            ld[r2] = L;
-            li[r2] = Li;
-            cnt[r2] = cr;
-            tau[r2] = th;
-          }
-        }
-        if (lane == 0 && p.merge_count) atomicAdd(p.merge_count + blockIdx.x, 1u);
-      } while (need);
-      wave_fence();
-    }
+    tile_candidates(p, c, bn, rid, live_mask, !more, S, bd, bi, t_app, t_fold);
     const uint64_t tb = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
-    t_fold += tb - tf;
     if (more) {
       store_tile(buf ^ 1, stage, stage_n);
       buf ^= 1;
@@ -418,16 +454,7 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     st[2] = t_fold;
     st[3] = t_bar;
   }
-  // write the per-(chunk, query) shortlist
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (qi < p.nq) {
-      const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
-      p.cand_d[o] = ld[r];
-      p.cand_i[o] = li[r];
-    }
-  }
+  store_shortlists(p, q0, chunk, S);
 }
 
 // Exact rescoring (l2_sqr_avx2 order, 8 lanes per row) of one query's shortlist.

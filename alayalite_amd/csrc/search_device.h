@@ -139,23 +139,27 @@ struct RowPass {
   float4 y[kR][kChunks];
 };
 
-// Issue every row chunk of the pass (all loads in flight before the first FMA).
+// Issue every row chunk of the pass (all loads in flight before the first FMA).  Branch-free: a
+// lane group past n loads the pass's first row again (its result is dropped), and a whole slot
+// past n is skipped wave-uniformly -- per-load exec-mask branches would serialise the issue.
+// Requires base < n.
 template <int kChunks>
 __device__ __forceinline__ void issue_rows(const SearchParams &p, const uint32_t *ids, int n, int base,
                                            RowPass<kChunks> &P) {
   constexpr int kRPL = RowPass<kChunks>::kR;
   const int lane = lane_id();
   const int g = lane >> 3, m = lane & 7;
+  const uint32_t id0 = ids[base];
 #pragma unroll
   for (int r = 0; r < kRPL; ++r) {
     const int idx = base + g + 8 * r;
     P.act[r] = idx < n;
-    P.id[r] = P.act[r] ? ids[idx] : 0u;
+    P.id[r] = P.act[r] ? ids[idx] : id0;
   }
 #pragma unroll
   for (int r = 0; r < kRPL; ++r) {
     const float4 *rp = reinterpret_cast<const float4 *>(p.base + static_cast<uint64_t>(P.id[r]) * p.stride) + m;
-    if (P.act[r]) {
+    if (base + 8 * r < n) {  // wave-uniform
 #pragma unroll
       for (int t = 0; t < kChunks; ++t) P.y[r][t] = rp[8 * t];
     } else {
@@ -328,6 +332,89 @@ constexpr int sq8_rows_per_group() {
   return kFull <= 0 ? 1 : (48 / kFull >= 4 ? 4 : (48 / kFull < 1 ? 1 : 48 / kFull));
 }
 
+// One pass of SQ8 code loads in registers (compile-time chunk count): lane group g takes rows
+// base + g + G r, r < kR.  Issued branch-free like issue_rows (a group past n reloads the pass's
+// first row, a whole slot past n is skipped wave-uniformly).
+template <int kOrder, int kFull>
+struct Sq8Pass {
+  static constexpr int P = kOrder == 2 ? 32 : 16;
+  static constexpr int LPR = P / 4;
+  static constexpr int G = 64 / LPR;
+  static constexpr int kR = sq8_rows_per_group<kOrder, kFull>();
+  static constexpr int kStep = G * kR;
+  uint32_t id[kR];
+  bool act[kR];
+  uint32_t w[kR][kFull > 0 ? kFull : 1];
+};
+
+template <int kOrder, int kFull>
+__device__ __forceinline__ void sq8_issue(const SearchParams &p, const uint32_t *ids, int n, int base,
+                                          Sq8Pass<kOrder, kFull> &S) {
+  static_assert(kFull > 0, "compile-time chunk count only");
+  using SP = Sq8Pass<kOrder, kFull>;
+  const int lane = lane_id();
+  const int g = lane / SP::LPR, m = lane % SP::LPR;
+  const uint32_t id0 = ids[base];
+#pragma unroll
+  for (int r = 0; r < SP::kR; ++r) {
+    const int idx = base + g + SP::G * r;
+    S.act[r] = idx < n;
+    S.id[r] = S.act[r] ? ids[idx] : id0;
+  }
+#pragma unroll
+  for (int r = 0; r < SP::kR; ++r) {
+    const uint8_t *row = p.codes + static_cast<uint64_t>(S.id[r]) * p.code_stride + 4 * m;
+    if (base + SP::G * r < n) {  // wave-uniform
+#pragma unroll
+      for (int t = 0; t < kFull; ++t) S.w[r][t] = *reinterpret_cast<const uint32_t *>(row + SP::P * t);
+    } else {
+#pragma unroll
+      for (int t = 0; t < kFull; ++t) S.w[r][t] = 0u;
+    }
+  }
+}
+
+template <bool kIP, int kOrder, int kFull>
+__device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *xq, const float *sc,
+                                           const float *mnv, int n, int base, Sq8Pass<kOrder, kFull> &S,
+                                           float *out) {
+  using SP = Sq8Pass<kOrder, kFull>;
+  constexpr int P = SP::P, LPR = SP::LPR, G = SP::G;
+  const int lane = lane_id();
+  const int g = lane / LPR, m = lane % LPR;
+  const int rem = static_cast<int>(p.dim) - P * kFull;
+  const bool half = rem >= P / 2;
+  const int tail_begin = P * kFull + (half ? P / 2 : 0);
+  float acc[SP::kR][4];
+#pragma unroll
+  for (int r = 0; r < SP::kR; ++r) {
+    acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0.f;
+    if (base + G * r >= n) break;  // wave-uniform
+#pragma unroll
+    for (int t = 0; t < kFull; ++t) sq8_chunk<kIP>(xq, sc, mnv, P * t + 4 * m, S.w[r][t], acc[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < SP::kR; ++r) {
+    if (base + G * r >= n) break;
+    const uint8_t *rw = p.codes + static_cast<uint64_t>(S.id[r]) * p.code_stride;
+    if (half && m < LPR / 2 && S.act[r])  // trailing half block -> acc[0 .. P/2)
+      sq8_chunk<kIP>(xq, sc, mnv, P * kFull + 4 * m, *reinterpret_cast<const uint32_t *>(rw + P * kFull + 4 * m),
+                     acc[r]);
+    float a0 = acc[r][0], a1 = acc[r][1], a2 = acc[r][2], a3 = acc[r][3];
+    if constexpr (kOrder == 2) {
+      a0 += lane_xor<4>(a0); a1 += lane_xor<4>(a1); a2 += lane_xor<4>(a2); a3 += lane_xor<4>(a3);
+    }
+    a0 += lane_xor<2>(a0); a1 += lane_xor<2>(a1); a2 += lane_xor<2>(a2); a3 += lane_xor<2>(a3);
+    a0 += lane_xor<1>(a0); a1 += lane_xor<1>(a1); a2 += lane_xor<1>(a2); a3 += lane_xor<1>(a3);
+    float res = kOrder == 2 ? (a0 + a2) + (a1 + a3) : (a0 + a1) + (a2 + a3);
+    if (S.act[r] && m == 0) {
+      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
+        res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(rw[e]), res);
+      out[base + g + G * r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
+    }
+  }
+}
+
 template <bool kIP, int kOrder, int kFull>
 __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float *xq,
                                               const float *sc, const float *mnv,
@@ -336,6 +423,15 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
   constexpr int LPR = P / 4;    // lanes per row
   constexpr int G = 64 / LPR;   // row groups per wave
   constexpr int kRPL = sq8_rows_per_group<kOrder, kFull>();
+  if constexpr (kFull > 0) {
+    for (int base = 0; base < n; base += G * kRPL) {
+      Sq8Pass<kOrder, kFull> S;
+      sq8_issue<kOrder, kFull>(p, ids, n, base, S);
+      sq8_finish<kIP, kOrder, kFull>(p, xq, sc, mnv, n, base, S, out);
+    }
+    wave_sync();
+    return;
+  }
   const int lane = lane_id();
   const int g = lane / LPR, m = lane % LPR;
   const int T = kFull > 0 ? kFull : static_cast<int>(p.dim) / P;

@@ -26,6 +26,180 @@ namespace alaya_amd {
 
 namespace {
 
+// LDS layout of a search workgroup (search_lds_bytes below is its size).
+template <int kSpace>
+__device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *smem) {
+  Lds L;
+  unsigned char *ptr = smem;
+  L.q = reinterpret_cast<float *>(ptr);
+  ptr += static_cast<size_t>(p.stride) * 4;
+  L.cid = reinterpret_cast<uint32_t *>(ptr);
+  ptr += 64 * 4;
+  L.cd = reinterpret_cast<float *>(ptr);
+  ptr += 64 * 4;
+  L.sd = reinterpret_cast<float *>(ptr);
+  ptr += 64 * 4;
+  L.pd = reinterpret_cast<float *>(ptr);
+  ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
+  L.pi = reinterpret_cast<uint32_t *>(ptr);
+  ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
+  L.hash = reinterpret_cast<uint32_t *>(ptr);
+  ptr += static_cast<size_t>(p.vis_rbits != kVisWide ? 2 : 4) << p.hash_log2;
+  L.sq_scale = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
+  ptr += kSpace ? static_cast<size_t>(p.stride) * 4 : 0;
+  L.sq_min = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
+  return L;
+}
+
+// Per-query setup shared by the search kernels: the query staged in LDS (SQ8: encoded with the
+// quantizer), visited table and pool cleared, then Graph::initialize_search (graph.hpp:148-158).
+template <bool kIP, int kChunks, int kSpace>
+__device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L, uint32_t qi, uint32_t *slot_bits,
+                                            uint64_t bit_words, Visited &vs, PoolState &ps,
+                                            uint32_t &n_dist_up, uint32_t &n_hops_up) {
+  const int lane = lane_id();
+  const uint32_t hsize = 1u << p.hash_log2;
+  // ---- per-query init ------------------------------------------------------------------
+  const float *qsrc = p.queries + static_cast<uint64_t>(qi) * p.q_stride;
+  if constexpr (kSpace == 0) {
+    for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
+  } else {
+    // SQ8Space::QueryComputer encodes the query with the quantizer (sq8_space.hpp:266-271,
+    // SQ8Quantizer::quantize sq8.hpp:118-130), then every distance uses its codes.
+    const float kInv255 = 1.0f / 255.0f;
+    for (uint32_t e = lane; e < p.stride; e += 64) {
+      float xq = 0.f, sc = 0.f, mn = 0.f;
+      if (e < p.dim) {
+        const float v = qsrc[e];
+        mn = p.sq_min[e];
+        const float mx = p.sq_max[e];
+        uint32_t code;
+        if (mx == mn) code = 0;
+        else if (v >= mx) code = 255;
+        else if (v <= mn) code = 0;
+        else code = static_cast<uint8_t>(((v - mn) / (mx - mn)) * 255);
+        sc = (mx - mn) * kInv255;
+        const float xf = static_cast<float>(code);
+        xq = kIP ? fmaf(xf, sc, mn) : xf;
+      }
+      L.q[e] = xq;
+      L.sq_scale[e] = sc;
+      L.sq_min[e] = mn;
+    }
+  }
+  {
+    const bool wide = p.vis_rbits == kVisWide;
+    const uint32_t words = wide ? hsize : hsize / 2;
+    for (uint32_t e = lane; e < words; e += 64) L.hash[e] = wide ? kEmpty : 0u;
+  }
+  for (uint32_t e = lane; e <= p.ef; e += 64) {
+    L.pd[e] = 0.f;
+    L.pi[e] = 0u;
+  }
+  wave_sync();
+  vs = make_visited(p, L.hash, slot_bits);
+  ps = PoolState{0u, 0u, p.ef};
+
+  // ---- Graph::initialize_search (graph.hpp:148-158) ---------------------------------------
+  if (p.levels != nullptr) {
+    // OverlayGraph::initialize (overlay_graph.hpp:122-144): greedy descent, strict '<'.
+    uint32_t u = p.ep;
+    if (lane == 0) L.cid[0] = u;
+    wave_sync();
+    space_distances<kIP, kChunks, kSpace>(p, L, L.cid, 1, L.cd);
+    float cur = L.cd[0];
+    ++n_dist_up;
+    for (int level = static_cast<int>(p.levels[u]); level > 0; --level) {
+      bool changed = true;
+      while (changed) {
+        changed = false;
+        const uint32_t *list = p.upper_edges + p.upper_off[u] +
+                               static_cast<uint64_t>(level - 1) * p.upper_R;
+        const uint32_t v = lane < static_cast<int>(p.upper_R) ? list[lane] : kEmpty;
+        const uint64_t endm = ballot(lane < static_cast<int>(p.upper_R) && v == kEmpty);
+        const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1
+                             : static_cast<int>(p.upper_R);
+        ++n_hops_up;
+        wave_sync();
+        if (lane < cnt) L.cid[lane] = v;
+        wave_sync();
+        space_distances<kIP, kChunks, kSpace>(p, L, L.cid, cnt, L.cd);
+        n_dist_up += cnt;
+        // first index of the minimum == the sequential strict-'<' scan's final choice
+        float dl = lane < cnt ? L.cd[lane] : FLT_MAX;
+        bool has = lane < cnt;
+        float mn = has ? dl : FLT_MAX;
+        for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+        const uint64_t at = ballot(has && dl == mn);
+        if (at && mn < cur) {
+          const int w = __ffsll(static_cast<unsigned long long>(at)) - 1;
+          u = read_lane(v, w);
+          cur = mn;
+          changed = true;
+        }
+        wave_sync();
+      }
+    }
+    // pool.insert(u, cur); vis.set(u)
+    if (lane == 0) {
+      L.pd[0] = cur;
+      L.pi[0] = u;
+    }
+    ps.size = 1;
+    ps.cur = 0;
+    visit(vs, u, lane == 0, bit_words);
+    wave_sync();
+  } else {
+    // NSG-style entry points: insert each ep, then mark it visited (graph.hpp:153-156)
+    for (uint32_t b = 0; b < p.n_eps; b += 64) {
+      const uint32_t cnt = min(64u, p.n_eps - b);
+      const bool has = static_cast<uint32_t>(lane) < cnt;
+      uint32_t v = has ? p.eps[b + lane] : 0u;
+      if (has) L.cid[lane] = v;
+      wave_sync();
+      for (uint32_t c = 0; c < cnt; c += 8) {
+        space_distances<kIP, kChunks, kSpace>(p, L, L.cid + c, min(8u, cnt - c), L.cd + c);
+      }
+      n_dist_up += cnt;
+      const float d = has ? L.cd[lane] : 0.f;
+      wave_sync();
+      pool_merge(ps, L, has, v, d);
+      // duplicates among eps are all inserted (no visited check in the reference loop)
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t vj = read_lane(v, j);
+        if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
+        visit(vs, vj, lane == 0, bit_words);
+      }
+      wave_sync();
+    }
+  }
+}
+
+// Results (ids[i] = pool.id(i), distances[i] = pool.dist(i), graph_search_job.hpp:254-256) and the
+// per-query counters.
+__device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, const PoolState &ps, uint32_t qi,
+                                          uint32_t n_dist, uint32_t n_expand, uint32_t n_dist_up,
+                                          uint32_t n_hops_up) {
+  const int lane = lane_id();
+  for (uint32_t i = lane; i < p.k; i += 64) {
+    uint32_t id = p.fill_id;
+    float d = p.fill_id == kEmpty ? FLT_MAX : 0.f;  // kEmpty fill (shard / corrected rerank) sorts last
+    if (i < ps.size) {
+      id = L.pi[i] & kIdMask;
+      d = L.pd[i];
+    }
+    p.out_ids[static_cast<uint64_t>(qi) * p.k + i] = id;
+    if (p.out_dists) p.out_dists[static_cast<uint64_t>(qi) * p.k + i] = d;
+  }
+  if (p.out_counters && lane == 0) {
+    uint32_t *c = p.out_counters + static_cast<uint64_t>(qi) * 4;
+    c[0] = n_dist;
+    c[1] = n_expand;
+    c[2] = n_dist_up;
+    c[3] = n_hops_up;
+  }
+}
+
 // --------------------------------------------------------------------------------------------
 // The search kernel.
 // --------------------------------------------------------------------------------------------
@@ -36,28 +210,7 @@ template <bool kIP, int kChunks, bool kStamp, int kSpace = 0>
 __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
-  Lds L;
-  {
-    unsigned char *ptr = smem;
-    L.q = reinterpret_cast<float *>(ptr);
-    ptr += static_cast<size_t>(p.stride) * 4;
-    L.cid = reinterpret_cast<uint32_t *>(ptr);
-    ptr += 64 * 4;
-    L.cd = reinterpret_cast<float *>(ptr);
-    ptr += 64 * 4;
-    L.sd = reinterpret_cast<float *>(ptr);
-    ptr += 64 * 4;
-    L.pd = reinterpret_cast<float *>(ptr);
-    ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
-    L.pi = reinterpret_cast<uint32_t *>(ptr);
-    ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
-    L.hash = reinterpret_cast<uint32_t *>(ptr);
-    ptr += static_cast<size_t>(p.vis_rbits != kVisWide ? 2 : 4) << p.hash_log2;
-    L.sq_scale = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
-    ptr += kSpace ? static_cast<size_t>(p.stride) * 4 : 0;
-    L.sq_min = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
-  }
-  const uint32_t hsize = 1u << p.hash_log2;
+  const Lds L = carve_lds<kSpace>(p, smem);
   const uint64_t bit_words = (p.n + 31) / 32;
   uint32_t *slot_bits = p.overflow_bits + static_cast<uint64_t>(blockIdx.x) * bit_words;
 
@@ -77,121 +230,10 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
         t_prev = now;
       }
     };
-    // ---- per-query init ------------------------------------------------------------------
-    const float *qsrc = p.queries + static_cast<uint64_t>(qi) * p.q_stride;
-    if constexpr (kSpace == 0) {
-      for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
-    } else {
-      // SQ8Space::QueryComputer encodes the query with the quantizer (sq8_space.hpp:266-271,
-      // SQ8Quantizer::quantize sq8.hpp:118-130), then every distance uses its codes.
-      const float kInv255 = 1.0f / 255.0f;
-      for (uint32_t e = lane; e < p.stride; e += 64) {
-        float xq = 0.f, sc = 0.f, mn = 0.f;
-        if (e < p.dim) {
-          const float v = qsrc[e];
-          mn = p.sq_min[e];
-          const float mx = p.sq_max[e];
-          uint32_t code;
-          if (mx == mn) code = 0;
-          else if (v >= mx) code = 255;
-          else if (v <= mn) code = 0;
-          else code = static_cast<uint8_t>(((v - mn) / (mx - mn)) * 255);
-          sc = (mx - mn) * kInv255;
-          const float xf = static_cast<float>(code);
-          xq = kIP ? fmaf(xf, sc, mn) : xf;
-        }
-        L.q[e] = xq;
-        L.sq_scale[e] = sc;
-        L.sq_min[e] = mn;
-      }
-    }
-    {
-      const bool wide = p.vis_rbits == kVisWide;
-      const uint32_t words = wide ? hsize : hsize / 2;
-      for (uint32_t e = lane; e < words; e += 64) L.hash[e] = wide ? kEmpty : 0u;
-    }
-    for (uint32_t e = lane; e <= p.ef; e += 64) {
-      L.pd[e] = 0.f;
-      L.pi[e] = 0u;
-    }
-    wave_sync();
-    Visited vs = make_visited(p, L.hash, slot_bits);
-    PoolState ps{0u, 0u, p.ef};
+    Visited vs;
+    PoolState ps;
     uint32_t n_dist = 0, n_expand = 0, n_dist_up = 0, n_hops_up = 0;
-
-    // ---- Graph::initialize_search (graph.hpp:148-158) ---------------------------------------
-    if (p.levels != nullptr) {
-      // OverlayGraph::initialize (overlay_graph.hpp:122-144): greedy descent, strict '<'.
-      uint32_t u = p.ep;
-      if (lane == 0) L.cid[0] = u;
-      wave_sync();
-      space_distances<kIP, kChunks, kSpace>(p, L, L.cid, 1, L.cd);
-      float cur = L.cd[0];
-      ++n_dist_up;
-      for (int level = static_cast<int>(p.levels[u]); level > 0; --level) {
-        bool changed = true;
-        while (changed) {
-          changed = false;
-          const uint32_t *list = p.upper_edges + p.upper_off[u] +
-                                 static_cast<uint64_t>(level - 1) * p.upper_R;
-          const uint32_t v = lane < static_cast<int>(p.upper_R) ? list[lane] : kEmpty;
-          const uint64_t endm = ballot(lane < static_cast<int>(p.upper_R) && v == kEmpty);
-          const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1
-                               : static_cast<int>(p.upper_R);
-          ++n_hops_up;
-          wave_sync();
-          if (lane < cnt) L.cid[lane] = v;
-          wave_sync();
-          space_distances<kIP, kChunks, kSpace>(p, L, L.cid, cnt, L.cd);
-          n_dist_up += cnt;
-          // first index of the minimum == the sequential strict-'<' scan's final choice
-          float dl = lane < cnt ? L.cd[lane] : FLT_MAX;
-          bool has = lane < cnt;
-          float mn = has ? dl : FLT_MAX;
-          for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
-          const uint64_t at = ballot(has && dl == mn);
-          if (at && mn < cur) {
-            const int w = __ffsll(static_cast<unsigned long long>(at)) - 1;
-            u = read_lane(v, w);
-            cur = mn;
-            changed = true;
-          }
-          wave_sync();
-        }
-      }
-      // pool.insert(u, cur); vis.set(u)
-      if (lane == 0) {
-        L.pd[0] = cur;
-        L.pi[0] = u;
-      }
-      ps.size = 1;
-      ps.cur = 0;
-      visit(vs, u, lane == 0, bit_words);
-      wave_sync();
-    } else {
-      // NSG-style entry points: insert each ep, then mark it visited (graph.hpp:153-156)
-      for (uint32_t b = 0; b < p.n_eps; b += 64) {
-        const uint32_t cnt = min(64u, p.n_eps - b);
-        const bool has = static_cast<uint32_t>(lane) < cnt;
-        uint32_t v = has ? p.eps[b + lane] : 0u;
-        if (has) L.cid[lane] = v;
-        wave_sync();
-        for (uint32_t c = 0; c < cnt; c += 8) {
-          space_distances<kIP, kChunks, kSpace>(p, L, L.cid + c, min(8u, cnt - c), L.cd + c);
-        }
-        n_dist_up += cnt;
-        const float d = has ? L.cd[lane] : 0.f;
-        wave_sync();
-        pool_merge(ps, L, has, v, d);
-        // duplicates among eps are all inserted (no visited check in the reference loop)
-        for (uint32_t j = 0; j < cnt; ++j) {
-          const uint32_t vj = read_lane(v, j);
-          if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
-          visit(vs, vj, lane == 0, bit_words);
-        }
-        wave_sync();
-      }
-    }
+    query_begin<kIP, kChunks, kSpace>(p, L, qi, slot_bits, bit_words, vs, ps, n_dist_up, n_hops_up);
 
     // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
     stamp(0);
@@ -252,24 +294,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       stamp(4);
     }
 
-    // ---- results (ids[i] = pool.id(i), distances[i] = pool.dist(i)) --------------------------
-    for (uint32_t i = lane; i < p.k; i += 64) {
-      uint32_t id = p.fill_id;
-      float d = p.fill_id == kEmpty ? FLT_MAX : 0.f;  // kEmpty fill (shard / corrected rerank) sorts last
-      if (i < ps.size) {
-        id = L.pi[i] & kIdMask;
-        d = L.pd[i];
-      }
-      p.out_ids[static_cast<uint64_t>(qi) * p.k + i] = id;
-      if (p.out_dists) p.out_dists[static_cast<uint64_t>(qi) * p.k + i] = d;
-    }
-    if (p.out_counters && lane == 0) {
-      uint32_t *c = p.out_counters + static_cast<uint64_t>(qi) * 4;
-      c[0] = n_dist;
-      c[1] = n_expand;
-      c[2] = n_dist_up;
-      c[3] = n_hops_up;
-    }
+    query_end(p, L, ps, qi, n_dist, n_expand, n_dist_up, n_hops_up);
     if constexpr (kStamp) {
       st[6] = __builtin_readcyclecounter() - t_begin;
       if (lane < 8) p.stamps[static_cast<uint64_t>(qi) * 8 + lane] = st[lane & 7];
