@@ -115,7 +115,7 @@ struct alaya_index {
   uint32_t code_stride = 0;
   DevBuf codes, sq_min, sq_max, rr_q_buf, sq_ids, sq_d;
   // flat path
-  DevBuf norms, cand_d, cand_i, flat_tau, flag_buf, iota;
+  DevBuf norms, cand_d, cand_i, flat_tau, flag_buf, iota, flat_q;
   bool norms_ready = false;
   float max_norm = 0.f;
   // scratch
@@ -340,12 +340,13 @@ void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStr
 }
 
 alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t *d_ids,
-                                  float *d_dists, uint32_t *d_flags, int *blocks) {
+                                  float *d_dists, uint32_t *d_flags, int *blocks, hipStream_t stream) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
   if (ix->metric != ALAYA_METRIC_L2) throw ArgError("the flat MFMA path supports the L2 metric");
   if (ix->generic) throw ArgError("the flat MFMA path ranks float32 rows (not the generic non-float order)");
-  if (alaya_amd::flat_scan_lds(ix->stride) == 0) throw ArgError("the flat MFMA path supports dim <= 224");
-  if (k == 0 || k > static_cast<uint32_t>(alaya_amd::flat_shortlist()) - 8) throw ArgError("flat search needs 1 <= k <= 24");
+  if (alaya_amd::flat_scan_lds(ix->stride) == 0) throw ArgError("no flat MFMA scan for this row stride");
+  if (k == 0 || k > static_cast<uint32_t>(alaya_amd::flat_max_k()))
+    throw ArgError("flat search needs 1 <= k <= " + std::to_string(alaya_amd::flat_max_k()));
   alaya_amd::FlatParams p{};
   p.base = ix->base.as<float>();
   p.n = ix->n;
@@ -360,6 +361,15 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
   p.queries = d_q;
   p.nq = nq;
   p.q_stride = ix->dim;
+  p.k_acc = ix->stride;
+  if (const uint32_t width = alaya_amd::flat_query_width(ix->stride)) {
+    // wide rows: the scan reads the queries as zero-padded rows of the slabbed width
+    ix->flat_q.reserve(nq * width * 4);
+    hip_check(alaya_amd::launch_pad_queries(d_q, nq, ix->dim, width, ix->flat_q.as<float>(), stream), "pad queries");
+    p.queries = ix->flat_q.as<float>();
+    p.q_stride = width;
+    p.k_acc = width;
+  }
   const int nqg = static_cast<int>((nq + 127) / 128);
   const int chunks = flat_chunks(ix, nqg, ix->n);
   p.n_chunks = chunks;
@@ -1352,7 +1362,7 @@ int alaya_index_flat_diag(alaya_index *ix, const float *d_queries, uint64_t nq, 
     scratch_acquire(ix, s);
     ensure_norms(ix, s);
     int blocks = 0;
-    alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
+    alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks, s);
     flat_prescan(ix, p, &blocks, s);
     p.ablate = ablate;
     p.merge_count = d_merge_count;
@@ -1372,7 +1382,7 @@ int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint
     scratch_acquire(ix, s);
     ensure_norms(ix, s);
     int blocks = 0;
-    alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks);
+    alaya_amd::FlatParams p = flat_params(ix, d_queries, nq, k, d_ids, d_dists, d_flags, &blocks, s);
     flat_prescan(ix, p, &blocks, s);
     hip_check(alaya_amd::launch_flat_scan(p, blocks, s), "flat scan");
     hip_check(alaya_amd::launch_flat_merge(p, s), "flat merge");
@@ -1397,7 +1407,7 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
     hip_check(hipMemcpyAsync(ix->q_buf.ptr, queries, nq * ix->dim * 4, hipMemcpyHostToDevice, ix->stream), "H2D");
     int blocks = 0;
     alaya_amd::FlatParams p = flat_params(ix, ix->q_buf.as<float>(), nq, k, ix->id_buf.as<uint32_t>(),
-                                          ix->dist_buf.as<float>(), ix->flag_buf.as<uint32_t>(), &blocks);
+                                          ix->dist_buf.as<float>(), ix->flag_buf.as<uint32_t>(), &blocks, ix->stream);
     flat_prescan(ix, p, &blocks, ix->stream);
     hip_check(alaya_amd::launch_flat_scan(p, blocks, ix->stream), "flat scan");
     hip_check(alaya_amd::launch_flat_merge(p, ix->stream), "flat merge");

@@ -11,14 +11,15 @@ struct FlatParams {
   const float *base;   // n x stride f32 rows (zero padded)
   uint64_t n;
   uint32_t dim;
-  uint32_t stride;     // multiple of 32, at most 256 for the MFMA scan
+  uint32_t stride;     // multiple of 32
   const float *norms;  // |b|^2 per row
   const uint32_t *valid;  // validity bitmap (bit i of word i/32), nullable = all rows valid;
                           // removed / invalid rows are never returned
   float max_norm;      // max |b|
-  const float *queries;
+  const float *queries;   // wide scan (flat_slab(stride) != 0): nq x flat_query_width(stride), zero padded
   uint64_t nq;
   uint32_t q_stride;
+  uint32_t k_acc;         // columns the scan accumulates over (stride, or the padded width)
   int n_chunks;        // base chunks (multiple of 8)
   float *cand_d;       // n_chunks x nq x shortlist approximate distances
   uint32_t *cand_i;
@@ -36,7 +37,14 @@ struct FlatParams {
 };
 
 int flat_shortlist();
+// largest k of the flat path (merged list of 256 with a margin of 32)
+int flat_max_k();
+// slab width of the wide scan for rows of `stride` floats (0: the narrow kernel, stride <= 224)
+uint32_t flat_slab(uint32_t stride);
+uint32_t flat_query_width(uint32_t stride);
 size_t flat_scan_lds(uint32_t stride);
+hipError_t launch_pad_queries(const float *src, uint64_t nq, uint32_t dim, uint32_t width, float *dst,
+                              hipStream_t s);
 hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, float *norms, hipStream_t s);
 hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s);
 hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s);

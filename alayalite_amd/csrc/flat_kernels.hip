@@ -34,6 +34,7 @@ constexpr int kL = 32;       // shortlist per (query, chunk)
 constexpr int kBuf = 96;     // candidate buffer per query
 constexpr int kTile = 32;    // base rows per LDS tile
 constexpr int kPad = 4;      // LDS row pitch padding (floats)
+constexpr int kWideTiles = 4;  // row tiles per super-chunk of the wide scan
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -145,10 +146,14 @@ __device__ __forceinline__ void fold32(float &L, uint32_t &Li, float cd, uint32_
 // half h holds the ascending list of query (r & 3) + 8 (r >> 2) + 4h, entry (lane & 31).  cnt[r] =
 // buffered candidates of that query (uniform over the half), tau[r] = its current 32nd distance;
 // full / nonempty: registers whose buffer holds >= kTile / > 0 candidates (uniform).
+// (vector values, not arrays: the fold picks a register by value, which the compiler turns into a
+// dynamic index -- on an array that means scratch memory, on a vector a register move)
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
 struct Shortlists {
-  float ld[16], tau[16];
-  uint32_t li[16];
-  int cnt[16];
+  f32x16 ld, tau;
+  u32x16 li;
+  i32x16 cnt;
   uint32_t full, nonempty;
 };
 
@@ -457,6 +462,207 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   store_shortlists(p, q0, chunk, S);
 }
 
+// --------------------------------------------------------------------------------------------
+// Wide rows (stride > 224): the queries' A fragments no longer fit in registers, so K is cut into
+// slabs of KS columns.  A super-chunk of TT row tiles keeps TT 32x32 accumulators; for each slab
+// the wave converts its 32 queries' KS-column A fragments (prefetched one slab ahead from a
+// zero-padded copy of the queries) and streams the super-chunk's (slab, tile) units through the
+// double-buffered LDS tile, slab-major.  After the last slab every tile of the super-chunk goes
+// through the same candidate handling (tile_candidates) as the narrow kernel, so shortlists, the
+// merge and its error bound are unchanged (the bound's gamma uses the padded length).
+// --------------------------------------------------------------------------------------------
+template <int KS, int TT, bool kSplit>
+__global__ void __launch_bounds__(256) flat_scan_wide_kernel(FlatParams p) {
+  static_assert(KS % 16 == 0 && KS <= 128, "slab width: a multiple of 16, at most 128");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int kPitch = KS + kPad;
+  constexpr int kBPitch = KS + 8;
+  constexpr int kTileWords = kSplit ? kTile * kBPitch : kTile * kPitch;
+  float *tile = reinterpret_cast<float *>(smem);  // 2 x kTileWords
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  float *bd = tile + 2 * kTileWords + wave * 32 * kBuf * 2;
+  uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kBuf);
+
+  const int nqg = static_cast<int>((p.nq + 127) / 128);
+  const int b = blockIdx.x;
+  const int qg = (b / 8) % nqg;
+  const int chunk = (b % 8) + 8 * (b / (8 * nqg));
+  if (chunk >= p.n_chunks) return;
+  const uint64_t rows_per_chunk = (p.n + p.n_chunks - 1) / p.n_chunks;
+  const uint64_t r0 = chunk * rows_per_chunk;
+  const uint64_t r1 = min(p.n, r0 + rows_per_chunk);
+  const int nslab = static_cast<int>((p.stride + KS - 1) / KS);
+  const uint32_t qwidth = static_cast<uint32_t>(nslab) * KS;  // padded query row (zeros past dim)
+
+  const uint64_t q0 = static_cast<uint64_t>(qg) * 128 + wave * 32;
+  // A prefetch: lane (col, h) holds query q0 + col, columns [s KS + h KS/2, + KS/2).  Queries past
+  // nq read the last query (their shortlists are never stored).
+  const uint64_t qa = min<uint64_t>(q0 + col, p.nq - 1);
+  const float4 *qrow = reinterpret_cast<const float4 *>(p.queries + qa * qwidth + h * (KS / 2));
+  float4 an[KS / 8];
+  auto load_a = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < KS / 8; ++j) an[j] = qrow[s * (KS / 4) + j];
+  };
+
+  Shortlists S;
+  init_shortlists(p, q0, h, S);
+
+  // cooperative unit load: 32 rows x KS columns, 256 threads, float4 each; rows past n read row
+  // n-1 (dead columns of the accumulator), columns past stride are zeroed when stored
+  constexpr int kVecPerRow = KS / 4;
+  constexpr int kPerThread = kTile * kVecPerRow / 256;
+  static_assert(kTile * kVecPerRow % 256 == 0, "whole float4s per thread");
+  auto load_unit = [&](uint64_t row0, uint32_t c0, float4 (&reg)[kPerThread]) {
+#pragma unroll
+    for (int v = 0; v < kPerThread; ++v) {
+      const int idx = threadIdx.x + v * 256;
+      const uint64_t row = min<uint64_t>(row0 + idx / kVecPerRow, p.n - 1);
+      const uint32_t c = min<uint32_t>(c0 + (idx % kVecPerRow) * 4, p.stride - 4);
+      reg[v] = *reinterpret_cast<const float4 *>(p.base + row * p.stride + c);
+    }
+  };
+  auto store_unit = [&](int buf, uint32_t c0, const float4 (&reg)[kPerThread]) {
+    float *t = tile + buf * kTileWords;
+#pragma unroll
+    for (int v = 0; v < kPerThread; ++v) {
+      const int idx = threadIdx.x + v * 256;
+      const bool in = c0 + (idx % kVecPerRow) * 4 < p.stride;
+      const float4 x = in ? reg[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (kSplit) {
+        __bf16 *th = reinterpret_cast<__bf16 *>(t) + (idx / kVecPerRow) * kBPitch + (idx % kVecPerRow) * 4;
+        bf16x4 hv, lv;
+        __bf16 hi, lo;
+        split_bf16(x.x, hi, lo); hv[0] = hi; lv[0] = lo;
+        split_bf16(x.y, hi, lo); hv[1] = hi; lv[1] = lo;
+        split_bf16(x.z, hi, lo); hv[2] = hi; lv[2] = lo;
+        split_bf16(x.w, hi, lo); hv[3] = hi; lv[3] = lo;
+        *reinterpret_cast<bf16x4 *>(th) = hv;
+        *reinterpret_cast<bf16x4 *>(th + kTile * kBPitch) = lv;
+      } else {
+        *reinterpret_cast<float4 *>(t + (idx / kVecPerRow) * kPitch + (idx % kVecPerRow) * 4) = x;
+      }
+    }
+  };
+
+  float4 stage[kPerThread];
+  load_a(0);
+  load_unit(r0, 0, stage);
+  store_unit(0, 0, stage);
+  __syncthreads();
+  int buf = 0;
+  uint64_t t_app = 0, t_fold = 0;
+  for (uint64_t sup = r0; sup < r1; sup += kTile * TT) {
+    const int ntiles = static_cast<int>(min<uint64_t>(TT, (r1 - sup + kTile - 1) / kTile));
+    const bool last_sup = sup + kTile * TT >= r1;
+    float bn[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) bn[t] = p.norms[min<uint64_t>(sup + kTile * t + col, p.n - 1)];
+    f32x16 c[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) c[t] = f32x16{};
+    for (int s = 0; s < nslab; ++s) {
+      // this slab's A fragments (k order as in the narrow kernel: k-step st of lane (col, h) holds
+      // columns s KS + h KS/2 + 8 st + j)
+      bf16x8 ah[kSplit ? KS / 16 : 1], al[kSplit ? KS / 16 : 1];
+      float a[kSplit ? 1 : KS / 2];
+      if constexpr (kSplit) {
+#pragma unroll
+        for (int st = 0; st < KS / 16; ++st) {
+          const float4 u = an[2 * st], w = an[2 * st + 1];
+          const float v8[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            __bf16 hi, lo;
+            split_bf16(v8[j], hi, lo);
+            ah[st][j] = hi;
+            al[st][j] = lo;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < KS / 8; ++j) {
+          a[4 * j] = an[j].x; a[4 * j + 1] = an[j].y; a[4 * j + 2] = an[j].z; a[4 * j + 3] = an[j].w;
+        }
+      }
+      const bool more_a = s + 1 < nslab || !last_sup;
+      if (more_a) load_a(s + 1 < nslab ? s + 1 : 0);  // next slab's fragments in flight
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        if (t < ntiles) {  // wave-uniform
+          // the unit after (s, t): (s, t+1), else (s+1, 0), else the next super-chunk's (0, 0)
+          uint64_t nrow = 0;
+          uint32_t ncol = 0;
+          bool next = true;
+          if (t + 1 < ntiles) {
+            nrow = sup + kTile * (t + 1);
+            ncol = s * KS;
+          } else if (s + 1 < nslab) {
+            nrow = sup;
+            ncol = (s + 1) * KS;
+          } else if (!last_sup) {
+            nrow = sup + kTile * TT;
+            ncol = 0;
+          } else {
+            next = false;
+          }
+          if (next) load_unit(nrow, ncol, stage);
+          if constexpr (kSplit) {
+            const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (KS / 2);
+#pragma unroll
+            for (int st = 0; st < KS / 16; ++st) {
+              const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * st);
+              const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * st);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[st], bh, c[t], 0, 0, 0);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c[t], 0, 0, 0);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c[t], 0, 0, 0);
+            }
+          } else {
+            const float *tp = tile + buf * kTileWords + col * kPitch + h * (KS / 2);
+#pragma unroll
+            for (int k = 0; k < KS / 2; k += 4) {
+              const float4 bv = *reinterpret_cast<const float4 *>(tp + k);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], bv.x, c[t], 0, 0, 0);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k + 1], bv.y, c[t], 0, 0, 0);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k + 2], bv.z, c[t], 0, 0, 0);
+              c[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k + 3], bv.w, c[t], 0, 0, 0);
+            }
+          }
+          if (next) {
+            store_unit(buf ^ 1, ncol, stage);
+            buf ^= 1;
+          }
+          __syncthreads();
+        }
+      }
+    }
+    // candidate handling of the super-chunk's tiles
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      if (t < ntiles) {
+        const uint64_t row0 = sup + kTile * t;
+        const uint32_t rid = static_cast<uint32_t>(row0 + col);
+        bool live = row0 + col < r1;
+        if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
+        const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
+        tile_candidates(p, c[t], bn[t], rid, live_mask, last_sup && t == ntiles - 1, S, bd, bi, t_app, t_fold);
+      }
+    }
+  }
+  store_shortlists(p, q0, chunk, S);
+}
+
+// zero-padded copy of the queries for the wide scan: dst[q][e] = src[q][e] for e < dim, else 0
+__global__ void pad_queries_kernel(const float *src, uint64_t nq, uint32_t dim, uint32_t width, float *dst) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nq * width) return;
+  const uint64_t q = i / width;
+  const uint32_t e = static_cast<uint32_t>(i % width);
+  dst[i] = e < dim ? src[q * dim + e] : 0.f;
+}
+
 // Exact rescoring (l2_sqr_avx2 order, 8 lanes per row) of one query's shortlist.
 __device__ float exact_l2(const FlatParams &p, const float *q, uint32_t id, int m) {
   const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
@@ -571,7 +777,7 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
     // (gamma x 3.1), and the dropped terms (ql.bl and the two split residuals) add
     // <= 3.02 * 2^-16 |q||b| to C, i.e. twice that to the distance; 1e-30 covers bf16 lo parts
     // flushed as denormals.
-    const float gam = 2.0f * static_cast<float>(p.stride) * 5.9604645e-8f * (p.split ? 3.1f : 1.0f);
+    const float gam = 2.0f * static_cast<float>(p.k_acc) * 5.9604645e-8f * (p.split ? 3.1f : 1.0f);
     const float qnorm = sqrtf(qn);
     const float bmax = p.max_norm;
     const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax) +
@@ -579,6 +785,171 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
     const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     wave_fence();
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Merge for k > kL - 8: the chunk shortlists are folded into a sorted list of M = 64R entries held
+// in registers (entry e = r * 64 + lane), by bitonic networks over (distance, id).  Every row
+// outside the list has approx >= cutoff = min(list[M-1], min over chunks of the chunk's 32nd, the
+// prescan threshold): a row outside its chunk's shortlist is at or above that chunk's 32nd, and a
+// listed row that lost the fold is at or above list[M-1].  The list is rescored exactly, sorted by
+// (exact distance, id), and the bound check of flat_merge_kernel runs on the k-th result.
+// --------------------------------------------------------------------------------------------
+// register-held lists of the big merge (vectors, so a computed index never becomes scratch)
+template <int R>
+using VF = float __attribute__((ext_vector_type(R)));
+template <int R>
+using VU = uint32_t __attribute__((ext_vector_type(R)));
+
+template <int R>
+__device__ __forceinline__ void cmpx_regs(VF<R> &d, VU<R> &ix, int r, int r2, bool up) {
+  // entries r (lower index) and r2 of the same lane; ascending when up
+  const bool sw = up ? before(d[r2], ix[r2], d[r], ix[r]) : before(d[r], ix[r], d[r2], ix[r2]);
+  const float td = d[r];
+  const uint32_t ti = ix[r];
+  d[r] = sw ? d[r2] : d[r];
+  ix[r] = sw ? ix[r2] : ix[r];
+  d[r2] = sw ? td : d[r2];
+  ix[r2] = sw ? ti : ix[r2];
+}
+
+// one stage (block size K, distance J) of a bitonic network over the 64R entries
+template <int R>
+__device__ __forceinline__ void bitonic_stage(VF<R> &d, VU<R> &ix, int K, int J) {
+  const int lane = lane_id();
+  if (J >= 64) {
+    const int rj = J >> 6;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if ((r & rj) == 0) cmpx_regs<R>(d, ix, r, r | rj, ((r * 64) & K) == 0);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = r * 64 + lane;
+      const bool up = (e & K) == 0;
+      const bool lower = (lane & J) == 0;
+      const float od = __shfl_xor(d[r], J);
+      const uint32_t oi = __shfl_xor(ix[r], J);
+      const bool o_first = before(od, oi, d[r], ix[r]);
+      const bool take = (up == lower) ? o_first : !o_first;  // lower slot of an ascending pair keeps the min
+      d[r] = take ? od : d[r];
+      ix[r] = take ? oi : ix[r];
+    }
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void bitonic_sort_big(VF<R> &d, VU<R> &ix) {
+#pragma unroll
+  for (int K = 2; K <= 64 * R; K <<= 1)
+#pragma unroll
+    for (int J = K >> 1; J > 0; J >>= 1) bitonic_stage<R>(d, ix, K, J);
+}
+
+// list (ascending) absorbs a sorted batch c: pair list[e] with c[M-1-e], keep the min (a bitonic
+// sequence holding the M smallest of both), then a bitonic merge
+template <int R>
+__device__ __forceinline__ void fold_big(VF<R> &L, VU<R> &Li, const VF<R> &c, const VU<R> &ci) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float rd = __shfl_xor(c[R - 1 - r], 63);
+    const uint32_t ri = __shfl_xor(ci[R - 1 - r], 63);
+    const bool take = before(rd, ri, L[r], Li[r]);
+    L[r] = take ? rd : L[r];
+    Li[r] = take ? ri : Li[r];
+  }
+#pragma unroll
+  for (int J = 32 * R; J > 0; J >>= 1) bitonic_stage<R>(L, Li, 64 * R, J);
+}
+
+template <int R>
+__global__ void __launch_bounds__(64) flat_merge_big_kernel(FlatParams p) {
+  constexpr int M = 64 * R;
+  constexpr int kPerFold = M / kL;  // chunk lists per fold
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float *q = reinterpret_cast<float *>(smem);
+  uint32_t *lid = reinterpret_cast<uint32_t *>(q + max(p.stride, p.q_stride));
+  float *led = reinterpret_cast<float *>(lid + M);
+  const int lane = lane_id();
+  for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
+    const float *qs = p.queries + qi * p.q_stride;
+    float qn = 0.f;
+    for (uint32_t e = lane; e < p.stride; e += 64) {
+      const float v = e < p.dim ? qs[e] : 0.f;
+      q[e] = v;
+      qn = fmaf(v, v, qn);
+    }
+    for (int off = 32; off > 0; off >>= 1) qn += __shfl_xor(qn, off);
+    VF<R> L;
+    VU<R> Li;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      L[r] = FLT_MAX;
+      Li[r] = 0xffffffffu;
+    }
+    float cmin = FLT_MAX;  // min over chunks of the chunk list's 32nd entry
+    for (int c0 = 0; c0 < p.n_chunks; c0 += kPerFold) {
+      VF<R> cd;
+      VU<R> ci;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int chunk = c0 + 2 * r + (lane >> 5);
+        cd[r] = FLT_MAX;
+        ci[r] = 0xffffffffu;
+        if (chunk < p.n_chunks) {
+          const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + (lane & 31);
+          cd[r] = p.cand_d[o];
+          ci[r] = p.cand_i[o];
+          if ((lane & 31) == kL - 1) cmin = fminf(cmin, cd[r]);
+        }
+      }
+      bitonic_sort_big<R>(cd, ci);
+      fold_big<R>(L, Li, cd, ci);
+    }
+    for (int off = 32; off > 0; off >>= 1) cmin = fminf(cmin, __shfl_xor(cmin, off));
+    const float lastv = __shfl(L[R - 1], 63);
+    const float cutoff = fminf(fminf(lastv, cmin), p.tau_init ? p.tau_init[qi] : FLT_MAX);
+#pragma unroll
+    for (int r = 0; r < R; ++r) lid[r * 64 + lane] = Li[r];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // exact distances of the list (8 lanes per row, 8 rows per pass)
+    const int g = lane >> 3, m = lane & 7;
+    for (int base = 0; base < M; base += 8) {
+      const uint32_t id = lid[base + g];
+      const bool ok = id != 0xffffffffu;
+      const float dd = exact_l2(p, q, ok ? id : 0u, m);
+      if (m == 0) led[base + g] = ok ? dd : FLT_MAX;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    VF<R> E;
+#pragma unroll
+    for (int r = 0; r < R; ++r) E[r] = led[r * 64 + lane];
+    bitonic_sort_big<R>(E, Li);  // by (exact distance, id)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t e = r * 64 + lane;
+      if (e < p.k) {
+        p.out_ids[qi * p.k + e] = Li[r];
+        if (p.out_dists) p.out_dists[qi * p.k + e] = E[r];
+      }
+    }
+    float kth_d = FLT_MAX;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if ((p.k - 1) / 64 == static_cast<uint32_t>(r)) kth_d = __shfl(E[r], (p.k - 1) & 63);
+    const float gam = 2.0f * static_cast<float>(p.k_acc) * 5.9604645e-8f * (p.split ? 3.1f : 1.0f);
+    const float qnorm = sqrtf(qn);
+    const float bmax = p.max_norm;
+    const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax) +
+                      (p.split ? 2.0f * 3.05f * 1.5258789e-5f * qnorm * bmax + 1e-30f : 0.0f);
+    const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
+    if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -628,6 +999,11 @@ size_t scan_lds() {
   return (2 * kTile * (K + 8) + 2 * kTile) * 4 + 4 * (32 * kBuf * 8);
 }
 
+template <int KS>
+size_t wide_lds() {
+  return (2 * kTile * (KS + 8)) * 4 + 4 * (32 * kBuf * 8);
+}
+
 }  // namespace
 
 int flat_shortlist() { return kL; }
@@ -638,7 +1014,28 @@ hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, floa
   return hipGetLastError();
 }
 
+uint32_t flat_slab(uint32_t stride) {
+  if (stride <= 224) return 0;  // narrow kernel: the whole row's A fragments stay in registers
+  // the slab width with the least zero padding, larger slabs first on ties
+  uint32_t best = 128;
+  uint64_t waste = ~0ull;
+  for (uint32_t ks : {128u, 96u, 64u}) {
+    const uint64_t w = (stride + ks - 1) / ks * ks - stride;
+    if (w < waste) {
+      waste = w;
+      best = ks;
+    }
+  }
+  return best;
+}
+
 size_t flat_scan_lds(uint32_t stride) {
+  switch (flat_slab(stride)) {
+    case 128: return wide_lds<128>();
+    case 96: return wide_lds<96>();
+    case 64: return wide_lds<64>();
+    default: break;
+  }
   switch (stride) {
     case 32: return scan_lds<32>();
     case 64: return scan_lds<64>();
@@ -647,13 +1044,40 @@ size_t flat_scan_lds(uint32_t stride) {
     case 160: return scan_lds<160>();
     case 192: return scan_lds<192>();
     case 224: return scan_lds<224>();
-    default: return 0;  // 256: double-buffered 32-row tile + shortlists exceed 160 KB of LDS
+    default: return 0;
   }
+}
+
+uint32_t flat_query_width(uint32_t stride) {
+  const uint32_t ks = flat_slab(stride);
+  return ks ? (stride + ks - 1) / ks * ks : 0;
+}
+
+hipError_t launch_pad_queries(const float *src, uint64_t nq, uint32_t dim, uint32_t width, float *dst,
+                              hipStream_t s) {
+  const uint64_t total = nq * width;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(pad_queries_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, s, src, nq,
+                     dim, width, dst);
+  return hipGetLastError();
 }
 
 hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
   const size_t lds = flat_scan_lds(p.stride);
   if (lds == 0) return hipErrorInvalidValue;
+  constexpr int TT = kWideTiles;
+  switch (flat_slab(p.stride)) {
+#define ALAYA_WIDE(KS)                                                                                  \
+  case KS:                                                                                              \
+    if (p.split)                                                                                        \
+      hipLaunchKernelGGL((flat_scan_wide_kernel<KS, TT, true>), dim3(blocks), dim3(256), lds, s, p);    \
+    else                                                                                                \
+      hipLaunchKernelGGL((flat_scan_wide_kernel<KS, TT, false>), dim3(blocks), dim3(256), lds, s, p);   \
+    return hipGetLastError();
+    ALAYA_WIDE(128) ALAYA_WIDE(96) ALAYA_WIDE(64)
+#undef ALAYA_WIDE
+    default: break;
+  }
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
     if (p.split)                                                                               \
@@ -676,10 +1100,22 @@ hipError_t launch_flat_threshold(const FlatParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
+int flat_max_k() { return 4 * 64 - 32; }
+
 hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s) {
-  const size_t lds = (static_cast<size_t>(p.stride) + 3 * kL + 2 * kBuf) * 4 + 64;
   const int grid = static_cast<int>(p.nq < 4096 ? p.nq : 4096);
-  hipLaunchKernelGGL(flat_merge_kernel, dim3(grid), dim3(64), lds, s, p);
+  if (p.k <= static_cast<uint32_t>(kL - 8)) {
+    const size_t lds = (static_cast<size_t>(std::max(p.stride, p.q_stride)) + 3 * kL + 2 * kBuf) * 4 + 64;
+    hipLaunchKernelGGL(flat_merge_kernel, dim3(grid), dim3(64), lds, s, p);
+  } else if (p.k <= 128 - 28) {
+    const size_t lds = (static_cast<size_t>(std::max(p.stride, p.q_stride)) + 2 * 128) * 4 + 64;
+    hipLaunchKernelGGL(flat_merge_big_kernel<2>, dim3(grid), dim3(64), lds, s, p);
+  } else if (p.k <= static_cast<uint32_t>(flat_max_k())) {
+    const size_t lds = (static_cast<size_t>(std::max(p.stride, p.q_stride)) + 2 * 256) * 4 + 64;
+    hipLaunchKernelGGL(flat_merge_big_kernel<4>, dim3(grid), dim3(64), lds, s, p);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -66,11 +66,47 @@ def test_flat_exact_scaled(native, orc, scale, shift):
     assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
 
 
+@pytest.mark.parametrize("n,d,nq,k", [(3000, 256, 20, 10), (2500, 300, 17, 10), (3000, 768, 12, 10),
+                                      (4000, 960, 10, 10), (2000, 960, 150, 24), (1500, 1000, 6, 5)])
+def test_flat_exact_wide_rows(native, orc, n, d, nq, k):
+    """Rows wider than the narrow scan's 224 floats: the slabbed scan (K cut into slabs, TT row
+    tiles per super-chunk, zero-padded queries) feeds the same shortlists and exact rescoring."""
+    rng = np.random.default_rng(n + d + k)
+    base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
+    q = np.ascontiguousarray(rng.random((nq, d), dtype=np.float32))
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, k)
+    ref_i, ref_d = _exact(orc, base, q, k)
+    assert np.array_equal(ids, ref_i)
+    assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+    if k <= 10:
+        # uniform 960-d distances concentrate: with k = 24 the gap to the 32nd shortlist entry can
+        # fall inside the split contraction's error bound, and those queries are recomputed
+        assert redo == 0
+
+
+@pytest.mark.parametrize("n,d,nq,k", [(6000, 128, 20, 50), (6000, 128, 9, 100), (5000, 64, 7, 224),
+                                      (4000, 960, 8, 100), (3000, 200, 5, 25)])
+def test_flat_exact_large_k(native, orc, n, d, nq, k):
+    """k past the 32-entry chunk shortlists: the merge folds them into a 128- or 256-entry
+    register list and proves the k-th result against min(list end, every chunk's 32nd)."""
+    rng = np.random.default_rng(3 * n + d + k)
+    base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
+    q = np.ascontiguousarray(rng.random((nq, d), dtype=np.float32))
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, k)
+    ref_i, ref_d = _exact(orc, base, q, k)
+    assert np.array_equal(ids, ref_i)
+    assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+
+
 def test_flat_rejects_unsupported(native):
     dev = native.DeviceIndex(0)
     dev.set_base(np.zeros((100, 300), np.float32), 0)
-    with pytest.raises(ValueError, match="dim <= 224"):
-        dev.flat_search(np.zeros((1, 300), np.float32), 10)
+    with pytest.raises(ValueError, match="k <= 224"):
+        dev.flat_search(np.zeros((1, 300), np.float32), 225)
 
 
 def test_flat_ties_and_fallback(native, orc):
