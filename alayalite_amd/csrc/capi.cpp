@@ -224,6 +224,13 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     while (l < lmax && (slot_bytes << (l + 1)) <= budget) ++l;
     return std::max<uint32_t>(10, std::min<uint32_t>(l, cap));
   };
+  if (mode == 0) {
+    // a 32-bit id table of >= 32 ef slots (load <= ~0.3 at the usual 10-24 visited ids per ef)
+    // costs one LDS atomic per probe instead of a load and a compare-and-swap: where it fits (the
+    // 1k-query SIFT shape) it is 11 % faster; a compact table stays the choice when LDS is short
+    const uint32_t wl = std::max<uint32_t>(10, ceil_log2(32ull * ef));
+    if (wl <= 15 && (static_cast<size_t>(4) << wl) <= budget) return set_mode(wl, false);
+  }
   if (mode != 2) {
     const uint32_t l = pick(2, 16);
     if (fits_compact(l)) return set_mode(l, true);

@@ -1,9 +1,9 @@
 """Kernel time on fixed, deterministic (device-built) graphs, for A/B across builds and search
 modes: SIFT 1M ef 85 (10k and 1k queries), GIST 1M ef 400 (1k), 768-d IP SQ8 1M ef 175 (1k).
 
-usage: python tools/time_fixed.py [--modes 1,2] [--only sift,gist,sq8,sift1k]
-Prints per workload and search mode (1 sequential, 2 pipelined) the mean launch time and a hash
-of the returned ids (equal hashes across modes = same results)."""
+usage: python tools/time_fixed.py [--visited 0,2] [--only sift,gist,sq8,sift1k]
+Prints per workload and visited-table mode (0 auto, 1 compact, 2 wide) the mean launch time and a
+hash of the returned ids (equal hashes across modes = same results)."""
 import argparse
 import os
 import sys
@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="1,2")
+    ap.add_argument("--visited", default="0")
     ap.add_argument("--only", default="sift,sift1k,gist,sq8")
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
@@ -26,7 +26,7 @@ def main():
 
     ext = _native._ext
     st = torch.cuda.current_stream()
-    modes = [int(m) for m in args.modes.split(",")]
+    modes = [int(m) for m in args.visited.split(",")]
     only = set(args.only.split(","))
     cache = {}
     for name, gen, nq, ef, metric, sq8 in (("sift", sift_like, 10000, 85, 0, False),
@@ -60,7 +60,7 @@ def main():
                 dev.search_device(qd.data_ptr(), nq, 10, ef, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(), st.cuda_stream)
 
         for mode in modes:
-            dev.set_search_mode(mode)
+            dev.set_visited_mode(mode)
             for _ in range(3):
                 run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -71,9 +71,9 @@ def main():
             torch.cuda.synchronize()
             h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
             c = cnt.cpu().numpy()
-            print(f"{name} mode {mode}: {e0.elapsed_time(e1) / args.reps:.4f} ms  ids-hash {h}  "
+            print(f"{name} visited {mode}: {e0.elapsed_time(e1) / args.reps:.4f} ms  ids-hash {h}  "
                   f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}", flush=True)
-        dev.set_search_mode(0)
+        dev.set_visited_mode(0)
 
 
 if __name__ == "__main__":
