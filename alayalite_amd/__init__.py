@@ -7,8 +7,8 @@ graph search, distance kernels, candidate pool and visited set run as hand-writt
 from .client import Client
 from .index import Index
 from .schema import IndexParams
-from .utils import calc_gt, calc_recall, load_fvecs, load_ivecs
+from .utils import calc_gt, calc_gt_device, calc_recall, load_fvecs, load_ivecs
 
-__all__ = ["Client", "Index", "IndexParams", "load_fvecs", "load_ivecs", "calc_recall", "calc_gt"]
+__all__ = ["Client", "Index", "IndexParams", "load_fvecs", "load_ivecs", "calc_recall", "calc_gt", "calc_gt_device"]
 
 __version__ = "0.1.0"

@@ -6,7 +6,7 @@ import hashlib
 
 import numpy as np
 
-__all__ = ["load_fvecs", "load_ivecs", "calc_recall", "calc_gt", "md5"]
+__all__ = ["load_fvecs", "load_ivecs", "calc_recall", "calc_gt", "calc_gt_device", "md5"]
 
 
 def _load_vecs(file_path, dtype):
@@ -43,6 +43,21 @@ def calc_gt(data, query, topk):
         d = np.linalg.norm(base - query[i].astype(np.float64), axis=1)
         gt[i] = np.argsort(d)[:topk]
     return gt
+
+
+def calc_gt_device(data, query, topk, device=0):
+    """Exact top-k L2 on the MI355X: the flat MFMA path (IndexType::FLAT has no implementation in the
+    reference; this is its exact search, find_exact_gt in include/utils/evaluate.hpp:29-62: the f32
+    l2_sqr metric, ties by id).  Any dimension, 1 <= topk <= 224.  Returns (ids int32, distances
+    float32).  Differs from calc_gt (float64 norms) only where two rows tie within f32 rounding."""
+    from . import _native
+
+    data = np.ascontiguousarray(data, dtype=np.float32)
+    query = np.ascontiguousarray(query, dtype=np.float32)
+    ix = _native._ext.DeviceIndex(device)
+    ix.set_base(data, 0)
+    ids, dists, _ = ix.flat_search(query, topk)
+    return ids.astype(np.int32), dists
 
 
 def md5(arr, chunk_size=1024 * 1024):

@@ -184,12 +184,13 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
 int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
                                         uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *d_ids,
                                         float *d_dists, uint32_t *d_counters, void *stream);
-/* ---- flat (exhaustive) exact k-NN, L2, dim <= 224, k <= 24 --------------------------------------
+/* ---- flat (exhaustive) exact k-NN, L2, any dim, 1 <= k <= 224 -----------------------------------
  * No reference implementation (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); the
  * analogue is find_exact_gt (include/utils/evaluate.hpp:29-62).  An MFMA pass ranks every row
  * by |b|^2 - 2 q.b and keeps a shortlist -- by default q.b from a bf16 hi/lo split (3 bf16 MFMAs,
  * error bounded and folded into the proof below); environment ALAYA_FLAT_F32=1 selects the f32
- * MFMA form.  The shortlist is rescored with the exact device metric
+ * MFMA form; rows wider than 224 floats are scanned in K slabs.  The shortlist (32 per row chunk,
+ * folded into a 128/256-entry list for k > 24) is rescored with the exact device metric
  * (l2_sqr_avx2 order) and sorted by (distance, id).  A query whose shortlist cannot be proven to
  * hold the exact top-k (error bound in flat_kernels.hip) is flagged; the host API recomputes it
  * exhaustively and reports how many it did. */

@@ -132,3 +132,17 @@ def test_flat_duplicates_sift_like(native, orc):
     ids, dists, redo = dev.flat_search(q, 10)
     ref_i, ref_d = _exact(orc, base, q, 10)
     assert np.array_equal(ids, ref_i) and np.array_equal(dists, ref_d)
+
+
+def test_calc_gt_device_matches_calc_gt(native):
+    """The public device helper (the flat path behind alayalite_amd.calc_gt_device) agrees with the
+    reference's float64 calc_gt (python/src/alayalite/utils.py:99-105) on continuous data."""
+    import alayalite_amd
+    from alayalite_amd.utils import calc_gt
+
+    rng = np.random.default_rng(31)
+    base = rng.random((4000, 300), dtype=np.float32)
+    q = rng.random((25, 300), dtype=np.float32)
+    ids, dists = alayalite_amd.utils.calc_gt_device(base, q, 10)
+    assert ids.dtype == np.int32 and dists.shape == (25, 10)
+    assert np.array_equal(ids, calc_gt(base, q, 10))
