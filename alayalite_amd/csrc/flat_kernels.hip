@@ -24,6 +24,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <cstdlib>
 
 #include "flat_kernels.h"
 
@@ -187,6 +188,7 @@ __device__ __forceinline__ void store_shortlists(const FlatParams &p, uint64_t q
 // Candidate handling of one 32-row tile: approximate distances a = |b|^2 - 2 c[r] below the
 // query's threshold are appended to its LDS buffer (bd/bi, a stack per query), then the fold
 // rounds that became due run.  last: the wave's final tile (every buffer is drained).
+template <int kB = kBuf>
 __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x16 &c, float bn, uint32_t rid,
                                                 uint64_t live_mask, bool last, Shortlists &S, float *bd,
                                                 uint32_t *bi, uint64_t &t_app, uint64_t &t_fold) {
@@ -210,14 +212,14 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x1
       const uint32_t hm = h ? static_cast<uint32_t>(mk >> 32) : static_cast<uint32_t>(mk);
       if (pass) {
         const int pos = S.cnt[r] + __popc(hm & ((1u << col) - 1u));
-        bd[qloc * kBuf + pos] = dv;
-        bi[qloc * kBuf + pos] = rid;
+        bd[qloc * kB + pos] = dv;
+        bi[qloc * kB + pos] = rid;
       }
       S.cnt[r] += __popc(hm);
       S.nonempty |= 1u << r;
       if (__builtin_amdgcn_ballot_w64(S.cnt[r] >= kTile)) {
         S.full |= 1u << r;
-        if (__builtin_amdgcn_ballot_w64(S.cnt[r] > kBuf - kTile)) need |= 1u << r;  // could overflow next tile
+        if (__builtin_amdgcn_ballot_w64(S.cnt[r] > kB - kTile)) need |= 1u << r;  // could overflow next tile
       }
     }
   }
@@ -263,8 +265,8 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x1
         float cd = FLT_MAX;
         uint32_t ci = 0xffffffffu;
         if (start + col < cr) {
-          cd = bd[qloc * kBuf + start + col];
-          ci = bi[qloc * kBuf + start + col];
+          cd = bd[qloc * kB + start + col];
+          ci = bi[qloc * kB + start + col];
         }
         fold32(L, Li, cd, ci, col);
         cr = start;
@@ -460,6 +462,147 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
     st[3] = t_bar;
   }
   store_shortlists(p, q0, chunk, S);
+}
+
+// --------------------------------------------------------------------------------------------
+// Narrow rows, warp-specialised (the default for stride <= 224, split contraction): 512 threads
+// = 4 producer waves + 4 consumer waves.  Producer wave w holds the A fragments of queries
+// 32w .. 32w+31, stages the block's 32-row tiles and turns each tile into its 32x32 contraction,
+// written to an LDS exchange buffer; consumer wave 4 + w runs the candidate handling (appends,
+// fold rounds, register shortlists -- tile_candidates, unchanged) on the previous tile's
+// contraction.  One barrier per step.  The waves of a pair share a SIMD, so the consumer's VALU
+// work issues in the gaps of the producer's MFMA chain instead of after it.
+// --------------------------------------------------------------------------------------------
+template <int K, int kB>
+__global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
+  static_assert(K % 16 == 0 && K <= 224, "narrow rows");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int kBPitch = K + 8;
+  constexpr int kTileWords = kTile * kBPitch;  // hi + lo bf16 half-tiles, 4-byte words per buffer
+  float *tile = reinterpret_cast<float *>(smem);                   // 2 x kTileWords
+  float *cx = tile + 2 * kTileWords;                                // 2 x 4 waves x 16 regs x 64 lanes
+  const int wave = threadIdx.x >> 6;
+  const int w = wave & 3;
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+
+  const int nqg = static_cast<int>((p.nq + 127) / 128);
+  const int b = blockIdx.x;
+  const int qg = (b / 8) % nqg;
+  const int chunk = (b % 8) + 8 * (b / (8 * nqg));
+  if (chunk >= p.n_chunks) return;
+  const uint64_t rows_per_chunk = (p.n + p.n_chunks - 1) / p.n_chunks;
+  const uint64_t r0 = chunk * rows_per_chunk;
+  const uint64_t r1 = min(p.n, r0 + rows_per_chunk);
+  const int ntiles = r1 > r0 ? static_cast<int>((r1 - r0 + kTile - 1) / kTile) : 0;
+  const uint64_t q0 = static_cast<uint64_t>(qg) * 128 + w * 32;
+
+  if (wave < 4) {
+    // ---- producer ------------------------------------------------------------------------
+    bf16x8 ah[K / 16], al[K / 16];
+    {
+      const uint64_t qi = q0 + col;
+      const uint32_t e0 = h * (K / 2);
+      const float *qp = p.queries + qi * p.q_stride;
+#pragma unroll
+      for (int s = 0; s < K / 16; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t e = e0 + 8 * s + j;
+          const float x = (qi < p.nq && e < p.dim) ? qp[e] : 0.f;
+          __bf16 hi, lo;
+          split_bf16(x, hi, lo);
+          ah[s][j] = hi;
+          al[s][j] = lo;
+        }
+    }
+    constexpr int kVecPerRow = K / 4;
+    constexpr int kVecs = kTile * kVecPerRow;
+    constexpr int kPerThread = (kVecs + 255) / 256;
+    auto load_tile = [&](uint64_t row0, float4 (&reg)[kPerThread]) {
+#pragma unroll
+      for (int v = 0; v < kPerThread; ++v) {
+        const int idx = threadIdx.x + v * 256;
+        reg[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (idx < kVecs) {
+          const uint64_t row = row0 + idx / kVecPerRow;
+          if (row < r1)
+            reg[v] = *reinterpret_cast<const float4 *>(p.base + row * p.row_step * p.stride + (idx % kVecPerRow) * 4);
+        }
+      }
+    };
+    auto store_tile = [&](int buf, const float4 (&reg)[kPerThread]) {
+      float *t = tile + buf * kTileWords;
+#pragma unroll
+      for (int v = 0; v < kPerThread; ++v) {
+        const int idx = threadIdx.x + v * 256;
+        if (idx < kVecs) {
+          __bf16 *th = reinterpret_cast<__bf16 *>(t) + (idx / kVecPerRow) * kBPitch + (idx % kVecPerRow) * 4;
+          bf16x4 hv, lv;
+          __bf16 hi, lo;
+          split_bf16(reg[v].x, hi, lo); hv[0] = hi; lv[0] = lo;
+          split_bf16(reg[v].y, hi, lo); hv[1] = hi; lv[1] = lo;
+          split_bf16(reg[v].z, hi, lo); hv[2] = hi; lv[2] = lo;
+          split_bf16(reg[v].w, hi, lo); hv[3] = hi; lv[3] = lo;
+          *reinterpret_cast<bf16x4 *>(th) = hv;
+          *reinterpret_cast<bf16x4 *>(th + kTile * kBPitch) = lv;
+        }
+      }
+    };
+    float4 stage[kPerThread];
+    load_tile(r0, stage);
+    store_tile(0, stage);
+    __syncthreads();
+    for (int s = 0; s <= ntiles; ++s) {
+      if (s < ntiles) {
+        const int buf = s & 1;
+        const bool more = s + 1 < ntiles;
+        if (more) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 1), stage);
+        f32x16 c = {};
+        const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
+#pragma unroll
+        for (int st = 0; st < K / 16; ++st) {
+          const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * st);
+          const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * st);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[st], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c, 0, 0, 0);
+        }
+        float *out = cx + ((buf * 4 + w) * 16) * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) out[r * 64] = c[r];
+        if (more) store_tile(buf ^ 1, stage);
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---- consumer ------------------------------------------------------------------------
+    float *bd = cx + 2 * 4 * 16 * 64 + w * 32 * kB * 2;  // 32 queries x kB
+    uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
+    Shortlists S;
+    init_shortlists(p, q0, h, S);
+    uint64_t t_app = 0, t_fold = 0;
+    __syncthreads();
+    for (int s = 0; s <= ntiles; ++s) {
+      if (s >= 1) {
+        const int t = s - 1;
+        const uint64_t row0 = r0 + static_cast<uint64_t>(kTile) * t;
+        const uint64_t row = row0 + col;
+        const uint32_t rid = static_cast<uint32_t>(row * p.row_step);
+        bool live = row < r1;
+        const float bn = p.norms[(live ? row : r0) * p.row_step];
+        if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
+        const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
+        const float *in = cx + (((t & 1) * 4 + w) * 16) * 64 + lane;
+        f32x16 c;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) c[r] = in[r * 64];
+        tile_candidates<kB>(p, c, bn, rid, live_mask, t == ntiles - 1, S, bd, bi, t_app, t_fold);
+      }
+      __syncthreads();
+    }
+    store_shortlists(p, q0, chunk, S);
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -999,6 +1142,14 @@ size_t scan_lds() {
   return (2 * kTile * (K + 8) + 2 * kTile) * 4 + 4 * (32 * kBuf * 8);
 }
 
+template <int K>
+constexpr int ws_buf() { return K >= 192 ? 64 : 80; }  // consumer buffers shrink to fit 160 KB
+
+template <int K>
+size_t ws_lds() {
+  return static_cast<size_t>(2 * kTile * (K + 8)) * 4 + 2 * 4 * 16 * 64 * 4 + 4 * (32 * ws_buf<K>() * 8);
+}
+
 template <int KS>
 size_t wide_lds() {
   return (2 * kTile * (KS + 8)) * 4 + 4 * (32 * kBuf * 8);
@@ -1078,9 +1229,15 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
 #undef ALAYA_WIDE
     default: break;
   }
+  // the warp-specialised kernel for the split contraction; the single-role kernel for the f32
+  // contraction and the diagnostics (ablation, per-phase stamps)
+  const bool ws = p.split && p.ablate == 0 && p.merge_count == nullptr && std::getenv("ALAYA_FLAT_WS0") == nullptr;
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
-    if (p.split)                                                                               \
+    if (ws)                                                                                    \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>()>), dim3(blocks), dim3(512),       \
+                         ws_lds<K>(), s, p);                                                   \
+    else if (p.split)                                                                          \
       hipLaunchKernelGGL((flat_scan_kernel<K, true>), dim3(blocks), dim3(256), lds, s, p);     \
     else                                                                                       \
       hipLaunchKernelGGL((flat_scan_kernel<K, false>), dim3(blocks), dim3(256), lds, s, p);    \

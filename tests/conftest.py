@@ -15,6 +15,14 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def native():
+    # torch (bundled HIP runtime) initialises the GPU before the engine's libamdhip64 does: the other
+    # order leaves torch without devices in tests that use torch streams (bench.py runs this order)
+    try:
+        import torch
+
+        torch.cuda.is_available()
+    except Exception:  # pragma: no cover - torch is optional for the engine itself
+        pass
     from alayalite_amd import _build
 
     _build.build()
