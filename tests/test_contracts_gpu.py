@@ -18,8 +18,9 @@ def _exact_valid(orc, base, q, k, valid_rows):
     return out
 
 
+@pytest.mark.parametrize("d,k", [(64, 10), (960, 10), (64, 50)])
 @pytest.mark.parametrize("f32", [False, True])
-def test_flat_skips_invalid_rows(native, orc, monkeypatch, f32):
+def test_flat_skips_invalid_rows(native, orc, monkeypatch, f32, d, k):
     """Rows cleared in the validity bitmap (removed rows) are never returned by the flat path, on
     the MFMA shortlist path and on the exhaustive recompute of a flagged query alike."""
     monkeypatch.delenv("ALAYA_FLAT_PRESCAN", raising=False)
@@ -28,7 +29,7 @@ def test_flat_skips_invalid_rows(native, orc, monkeypatch, f32):
     else:
         monkeypatch.delenv("ALAYA_FLAT_F32", raising=False)
     rng = np.random.default_rng(31)
-    n, d = 3000, 64
+    n = 3000  # d = 64: the warp-specialised (split) or single-role (f32) scan; 960: the slabbed scan
     base = rng.random((n, d), dtype=np.float32)
     q = rng.random((12, d), dtype=np.float32)
     # invalidate each query's 5 nearest rows plus a block of rows
@@ -40,8 +41,8 @@ def test_flat_skips_invalid_rows(native, orc, monkeypatch, f32):
     bitmap = np.packbits(valid_rows.astype(np.uint8), bitorder="little")
     dev = native.DeviceIndex(0)
     dev.set_base(base, 0, bitmap)
-    ids, dists, _ = dev.flat_search(q, 10)
-    for a, (ri, rd) in enumerate(_exact_valid(orc, base, q, 10, valid_rows)):
+    ids, dists, _ = dev.flat_search(q, k)
+    for a, (ri, rd) in enumerate(_exact_valid(orc, base, q, k, valid_rows)):
         assert np.array_equal(ids[a], ri), a
         assert np.array_equal(dists[a].view(np.uint32), rd.view(np.uint32)), a
     # all-tied rows force the exhaustive recompute: still only valid rows
