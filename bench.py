@@ -316,6 +316,17 @@ def recall(ids, gt):
     return hits / float(ids.size)
 
 
+def flat_scan_kernel_name(dim):
+    """The scan kernel launch_flat_scan (csrc/flat_kernels.hip) dispatches for rows of `dim` floats:
+    the slabbed wide scan past 224 columns, else the warp-specialised split scan unless the f32
+    contraction or the single-role scan is forced by environment."""
+    if (dim + 31) // 32 * 32 > 224:
+        return "flat_scan_wide_kernel"
+    if os.environ.get("ALAYA_FLAT_F32") or os.environ.get("ALAYA_FLAT_WS0"):
+        return "flat_scan_kernel"
+    return "flat_scan_ws_kernel"
+
+
 def run_flat(args):
     """BASELINE config 2: flat exact k-NN, 1M x 128 U[0,1) (seeds 1/2), 1k queries, k=10, MFMA."""
     import torch
@@ -369,13 +380,18 @@ def run_flat(args):
         ok += int(set(r.tolist()) == set(got[qi].tolist()))
     flops = 2.0 * n * nq * dim
     tf = flops / (ms * 1e-3) / 1e12
-    # HBM traffic of the scan from the committed PMC passes on this workload (tools/run_pmc_flat.sh)
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01", "traffic_flat.json")
-    if os.path.exists(tpath):
+    scan = flat_scan_kernel_name(dim)
+    # HBM traffic of the scan from the committed PMC passes on this workload and kernel
+    # (tools/run_pmc_flat.sh; latest round first)
+    import glob
+
+    traffic = tsrc = None
+    for tpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_flat*.json")), reverse=True):
         t = json.load(open(tpath))
-        if t.get("config", {}).get("n_base") == n and t["config"].get("n_queries") == nq and t["config"].get("dim") == dim:
-            traffic = t
+        c = t.get("config", {})
+        if (c.get("n_base"), c.get("n_queries"), c.get("dim"), t.get("kernel")) == (n, nq, dim, scan):
+            traffic, tsrc = t, os.path.relpath(tpath, ROOT)
+            break
     cpu = None
     if not args.no_cpu_baseline:  # find_exact_gt restated (oracle/), a bounded sample of the queries
         import oracle
@@ -402,10 +418,10 @@ def run_flat(args):
         "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
                      "frac": round(tf / 157.3, 4),
                      "traffic": round(traffic["traffic_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1) if traffic else None,
-                     "traffic_unit": "GB/s (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE of flat_scan_kernel)",
+                     "traffic_unit": f"GB/s (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE of {scan})",
                      "traffic_bytes_per_launch": int(traffic["traffic_bytes_per_launch"]) if traffic else None,
-                     "traffic_source": "profiles/r01/traffic_flat.json" if traffic else None,
-                     "kernel": "flat_scan_kernel+flat_merge_kernel",
+                     "traffic_source": tsrc,
+                     "kernel": f"{scan}+flat_merge_kernel",
                      "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops,
                      # the default contraction issues 3 bf16 MFMAs per f32 product (hi/lo split):
                      # its own ceiling is the 2.5 PF bf16 peak / 3, which the scan is far from --

@@ -5,32 +5,40 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KB) counts 128 B req
 wide coalesced reads -> bytes_read = 2 * FETCH_SIZE * 1024 (cross-checked: TCC_EA0_RDREQ_sum * 64
 equals FETCH_SIZE * 1024 when TCC_EA0_RDREQ_32B_sum == 0).  WRITE_SIZE (KB) is taken as is.
 usage: python tools/pmc_summary.py gpurun_out profiles/r01/traffic.json [flat]
-  (flat: tools/run_pmc_flat.sh's flat_scan_kernel passes; algorithmic bytes = the base read once)
+  (flat: tools/run_pmc_flat.sh's flat scan kernel passes; algorithmic bytes = the base read once)
 """
 
 import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
 def per_launch(path, kernel="hnsw_search_kernel"):
     vals = {}
+    names = set()
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+            names.add(re.search(r"\w*" + kernel + r"\w*", r["Kernel_Name"]).group(0))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}, names
 
 
 def main(src, dst, mode="hnsw"):
     c = {}
     launches = {}
-    prefix, kernel = ("pmcf_", "flat_scan_kernel") if mode == "flat" else ("pmc_", "hnsw_search_kernel")
+    # flat: whichever scan kernel the dispatch picked (flat_scan_kernel / _ws_kernel / _wide_kernel)
+    prefix, kernel = ("pmcf_", "flat_scan_") if mode == "flat" else ("pmc_", "hnsw_search_kernel")
+    names = set()
     for f in glob.glob(os.path.join(src, prefix + "*", "run_counter_collection.csv")):
-        v, n = per_launch(f, kernel)
+        v, n, nm = per_launch(f, kernel)
         c.update(v)
         launches.update(n)
+        names |= nm
+    if len(names) > 1:
+        sys.exit(f"passes profiled different kernels: {sorted(names)}")
     cfg = json.load(open(os.path.join(src, prefix + "FETCH_SIZE.json")))
     read_b = 2.0 * c["FETCH_SIZE"] * 1024.0
     write_b = c.get("WRITE_SIZE", 0.0) * 1024.0
@@ -42,7 +50,7 @@ def main(src, dst, mode="hnsw"):
     hit = c.get("TCC_HIT_sum", 0.0)
     miss = c.get("TCC_MISS_sum", 0.0)
     out = {
-        "kernel": kernel,
+        "kernel": names.pop() if names else kernel,
         "config": {k: cfg["config"][k] for k in ("n_base", "n_queries", "dim", "k", "ef_search") if k in cfg["config"]},
         "launches_per_pass": launches,
         "counters_per_launch": c,
