@@ -53,6 +53,8 @@ def build(force: bool = False, verbose: bool = False) -> tuple[str, str]:
                      f"-I{INCLUDE}", "-c", os.path.join(CSRC, src), "-o", obj]
             if src.endswith(".hip"):
                 flags[1:1] = ["-x", "hip", f"--offload-arch={ARCH}"]
+                # diagnostic builds only (e.g. -DALAYA_FINE_STAMPS for tools/profile_phases.py)
+                flags[1:1] = os.environ.get("ALAYA_EXTRA_HIPFLAGS", "").split()
             if verbose:
                 print(" ".join(flags), flush=True)
             procs.append((subprocess.Popen(flags), flags))

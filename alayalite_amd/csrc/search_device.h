@@ -690,9 +690,13 @@ struct NoNext {
 
 // on_next(id) is called (wave-uniformly, before the shift) when the closest accepted candidate
 // lands at or before the first unchecked entry, i.e. when it is the next pop.
-template <typename OnNext = NoNext>
+struct NoMark {
+  __device__ void operator()() const {}
+};
+
+template <typename OnNext = NoNext, typename Mark = NoMark>
 __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d,
-                           OnNext on_next = OnNext()) {
+                           OnNext on_next = OnNext(), Mark mark = Mark()) {
   const int lane = lane_id();
   const bool full = ps.size == ps.ef;
   const float last = full ? L.pd[ps.size - 1] : 0.f;
@@ -716,6 +720,7 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   const int lane0 = __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1;
   const uint32_t first_pos = read_lane(pos, lane0);
   if (first_pos <= ps.cur) on_next(read_lane(id, lane0));
+  mark();  // diagnostics: end of the rank / position phase
   wave_sync();
   // shift pool entries [first_pos, size) up by #accepted strictly smaller, top chunk first.
   for (int hi = static_cast<int>(ps.size); hi > static_cast<int>(first_pos); hi -= 64) {

@@ -244,18 +244,25 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     while (ps.cur < ps.size) {
       const uint32_t u = pool_pop(ps, L);
       ++n_expand;
+#ifndef ALAYA_FINE_STAMPS
       if (kStamp && vs.spilled) st[5]++;
+#endif
       stamp(1);
       uint32_t v;
       if (u == pred) {
         v = pred_v;
+#ifndef ALAYA_FINE_STAMPS
         if (kStamp) st[7]++;
+#endif
       } else {
         v = lane < static_cast<int>(p.R) ? p.l0[static_cast<uint64_t>(u) * p.R + lane] : kEmpty;
       }
       const uint64_t endm = ballot(lane < static_cast<int>(p.R) && v == kEmpty);
       const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1 : static_cast<int>(p.R);
       bool act = lane < cnt;
+#ifdef ALAYA_FINE_STAMPS
+      stamp(2);
+#endif
       if (p.dedup_edges) {  // graphs with repeated ids in a row: keep the first occurrence only
         for (int j = 0; j < cnt; ++j) {
           const uint32_t vj = read_lane(v, j);
@@ -270,7 +277,11 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
       // otherwise wait for that load too (vmcnt counts in issue order)
       pred = ps.cur < ps.size ? (L.pi[ps.cur] & kIdMask) : kEmpty;
       if (pred != kEmpty && lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(pred) * p.R + lane];
+#ifdef ALAYA_FINE_STAMPS
+      stamp(5);
+#else
       stamp(2);
+#endif
       if (nf == 0) continue;
       // compact fresh ids in adjacency order
       const uint32_t slot = __popcll(fm & ((1ull << lane) - 1ull));
@@ -290,7 +301,11 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
           pred = nx;
           if (lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(nx) * p.R + lane];
         }
-      });
+      }
+#ifdef ALAYA_FINE_STAMPS
+      , [&]() { stamp(7); }
+#endif
+      );
       stamp(4);
     }
 

@@ -43,20 +43,36 @@ R = 32
 # HNSW workloads (BASELINE.json configs; generators and seeds in workloads/datasets.py)
 WORKLOADS = {
     "gist-hnsw": {"gen": "gist_like", "dim": 960, "nq": 1000, "metric": 0, "sq8": False,
-                  "metric_name": "QPS @ recall@10>=0.95, GIST-960 L2, 1M base / 1k queries",
+                  "metric_name": "QPS @ recall@10>=0.95, GIST-960 L2, {base} base / {queries} queries",
+                  "config_tag": {(1_000_000, 1000): "", (1_000_000, 10000): " (config 4)"},
                   "data": "synthetic (GIST-shaped 1024-centre low-rank mixture, seeds 5/6; graph built by the "
                           "engine's HNSW builder R=32 efc=100)"},
     "sift-hnsw": {"gen": "sift_like", "dim": 128, "nq": 10000, "metric": 0, "sq8": False,
-                  "metric_name": "QPS @ recall@10>=0.95, SIFT-128 L2, 1M base / 10k queries (config 3)",
+                  "metric_name": "QPS @ recall@10>=0.95, SIFT-128 L2, {base} base / {queries} queries",
+                  "config_tag": {(1_000_000, 10000): " (config 3)"},
                   "data": "synthetic (SIFT-shaped 1024-centre mixture, integer-valued, seeds 3/4; graph built by "
                           "the engine's HNSW builder R=32 efc=100)"},
     "sq8-ip": {"gen": "text_like", "dim": 768, "nq": 1000, "metric": 1, "sq8": True, "n": 10_000_000,
-               "metric_name": "QPS @ recall@10>=0.95, 768-d IP, SQ8 search + f32 rerank, 10M base / 1k queries "
-                              "(config 5)",
+               "metric_name": "QPS @ recall@10>=0.95, 768-d IP, SQ8 search + f32 rerank, {base} base / {queries} "
+                              "queries",
+               "config_tag": {(10_000_000, 1000): " (config 5)", (10_000_000, 10000): " (config 5)"},
                "data": "synthetic (text-embedding-shaped 4096-centre unit-sphere mixture, 12 latent dims, "
                        "row-normalised, seeds 7/8; graph built on f32 rows with IP, R=32 efc=100; SQ8 codes of the "
                        "same rows)"},
 }
+
+
+def _count(v):
+    for unit, div in (("M", 1_000_000), ("k", 1000)):
+        if v >= div and v % div == 0:
+            return f"{v // div}{unit}"
+    return str(v)
+
+
+def metric_label(w, n, nq):
+    """The workload's metric string for this base / query count (the BASELINE metric at its own
+    shape, e.g. "QPS @ recall@10>=0.95, GIST-960 L2, 1M base / 1k queries")."""
+    return w["metric_name"].format(base=_count(n), queries=_count(nq)) + w["config_tag"].get((n, nq), "")
 
 
 def log(*a):
@@ -669,7 +685,7 @@ def main():
     if rank == 0:
         r_at = next((s["recall"] for s in sweep if s["ef"] == ef), None)
         out = {
-            "metric": w["metric_name"],
+            "metric": metric_label(w, args.n, nq),
             "value": round(value, 1),
             "unit": "queries/s",
             "n_gpus": world,

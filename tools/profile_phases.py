@@ -29,9 +29,18 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--workload", choices=("gist", "sq8", "sift"), default="gist",
                     help="sq8: config-5 data (768-d IP, device-built graph), stamped SQ8 traversal")
+    ap.add_argument("--fine", action="store_true",
+                    help="the package was built with -DALAYA_FINE_STAMPS (ALAYA_EXTRA_HIPFLAGS): slots split "
+                         "the adjacency wait from the visited phase and the merge's rank/position phase from "
+                         "its shift")
     args = ap.parse_args()
-    import bench as b
+    import bench as b  # (puts the tree first on sys.path)
+
+    if os.environ.get("ALAYA_AB_ROOT"):  # a saved (e.g. diagnostic) build of the package instead of the tree's
+        sys.path.insert(0, os.environ["ALAYA_AB_ROOT"])
     from alayalite_amd import _native
+
+    print("engine:", os.path.dirname(_native.__file__), flush=True)
     from workloads.datasets import gist_like
 
     ext = _native._ext
@@ -59,10 +68,13 @@ def main():
             dev.set_graph(g)
     else:
         base, queries = gist_like(args.n, args.nq, args.dim)
-        g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
         dev = ext.DeviceIndex(0)
         dev.set_base(base, 0)
-        dev.set_graph(g)
+        if args.builder == "gpu":
+            dev.build_graph(32, 100, 100, 0, 0, 2)
+        else:
+            g, _ = b.graph_for(ext, base, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), "gist")
+            dev.set_graph(g)
     if args.hash_log2:
         dev.set_hash_log2(args.hash_log2)
     if args.visited_mode:
@@ -79,6 +91,9 @@ def main():
     ids, cnt, st = dev.profile_search(queries, 10, args.ef, space)
     assert np.array_equal(ids, ids0)
     names = ["init+descent", "pop", "adj+visited", "distances", "merge", "spilled_expansions", "query_total"]
+    if args.fine:
+        names = ["init+descent", "pop", "adjacency wait", "distances", "merge shift+tail", "visited+prefetch",
+                 "query_total", "merge rank+position"]
     mean = st.mean(0)
     exp = cnt[:, 1].mean()
     print(f"n={args.n} ef={args.ef} nq={args.nq} host-timed plain search {plain*1e3:.2f} ms "
@@ -86,8 +101,20 @@ def main():
     for i, nme in enumerate(names):
         per = mean[i] / exp if i not in (5, 6) else mean[i]
         print(f"  {nme:20s} mean/query {mean[i]:14.1f}   per expansion {mean[i]/exp:10.1f}")
-    print(f"  adjacency prefetch hits {mean[7]:.1f} per query = {mean[7] / exp:.3f} of expansions")
+    if not args.fine:
+        print(f"  adjacency prefetch hits {mean[7]:.1f} per query = {mean[7] / exp:.3f} of expansions")
     print(f"  max query_total {st[:,6].max()}  min {st[:,6].min()}  p50 {np.median(st[:,6])}")
+    # the launch ends with its slowest query: is the tail more expansions or slower expansions?
+    ne = cnt[:, 1].astype(np.float64)
+    tot = st[:, 6].astype(np.float64)
+    q = [50, 90, 99, 100]
+    print("  n_expand percentiles p50/p90/p99/max", [float(np.percentile(ne, x)) for x in q])
+    print("  n_dist   percentiles p50/p90/p99/max", [float(np.percentile(cnt[:, 0], x)) for x in q])
+    print("  cycles per expansion p50/p90/p99/max", [round(float(np.percentile(tot / ne, x)), 1) for x in q])
+    slow = np.argsort(tot)[-5:]
+    print("  slowest 5 queries: cycles", tot[slow].astype(np.int64).tolist(), "n_expand", ne[slow].astype(int).tolist(),
+          "n_dist", cnt[slow, 0].tolist())
+    print(f"  corr(cycles, n_expand) {np.corrcoef(tot, ne)[0, 1]:.3f}")
     if args.out:
         np.save(args.out, st)
 

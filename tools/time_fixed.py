@@ -12,6 +12,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if os.environ.get("ALAYA_AB_ROOT"):  # A/B: a saved build of the package (e.g. ab/base) instead of the tree's
+    sys.path.insert(0, os.environ["ALAYA_AB_ROOT"])
 
 
 def main():
@@ -25,6 +27,7 @@ def main():
     from workloads.datasets import gist_like, sift_like, text_like
 
     ext = _native._ext
+    print("engine:", os.path.dirname(_native.__file__), flush=True)
     st = torch.cuda.current_stream()
     modes = [int(m) for m in args.visited.split(",")]
     only = set(args.only.split(","))
