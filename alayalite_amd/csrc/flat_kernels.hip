@@ -468,19 +468,52 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
 // Narrow rows, warp-specialised (the default for stride <= 224, split contraction): 512 threads
 // = 4 producer waves + 4 consumer waves.  Producer wave w holds the A fragments of queries
 // 32w .. 32w+31, stages the block's 32-row tiles and turns each tile into its 32x32 contraction,
-// written to an LDS exchange buffer; consumer wave 4 + w runs the candidate handling (appends,
-// fold rounds, register shortlists -- tile_candidates, unchanged) on the previous tile's
-// contraction.  One barrier per step.  The waves of a pair share a SIMD, so the consumer's VALU
-// work issues in the gaps of the producer's MFMA chain instead of after it.
+// written to slot t % kD of an LDS ring; consumer wave 4 + w runs the candidate handling (appends,
+// fold rounds, register shortlists -- tile_candidates, unchanged) on the contractions in order.
+// The waves of a pair share a SIMD, so the consumer's VALU work issues in the gaps of the
+// producer's MFMA chain.  No block-wide barrier per tile: a pair hands tiles over through LDS
+// flags (producer w publishes tile t, consumer w acknowledges it), and only the four producers
+// meet per tile (an LDS counter) because they stage the shared tile together.  A consumer that
+// draws a fold round falls up to kD - 1 tiles behind its producer instead of stalling all eight
+// waves at a barrier (the fold rounds of the four consumers fall on different tiles).
 // --------------------------------------------------------------------------------------------
-template <int K, int kB>
+constexpr uint32_t kSpinLimit = 1u << 20;  // ~0.1 s of polling: a protocol error ends the scan, not the GPU
+
+// Wait until *a >= v (wave-uniform).  False when the block aborted (a wait ran past kSpinLimit):
+// every later wait then returns at once, the loops end and the shortlists are written as
+// unprovable (see flat_scan_ws_kernel), so the merge flags the queries for the exhaustive redo.
+__device__ __forceinline__ bool lds_wait_ge(uint32_t *a, uint32_t v, uint32_t *abort) {
+  for (uint32_t n = 0;; ++n) {
+    if (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) break;
+    if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) return false;
+    if (n == kSpinLimit) {
+      if (__lane_id() == 0) __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");  // later LDS reads after the flag
+  return true;
+}
+// Publish v in *a after this wave's earlier LDS writes (LDS operations of a wave complete in order).
+__device__ __forceinline__ void lds_publish(uint32_t *a, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (__lane_id() == 0) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int K, int kB, int kD>
 __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
   static_assert(K % 16 == 0 && K <= 224, "narrow rows");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int kBPitch = K + 8;
   constexpr int kTileWords = kTile * kBPitch;  // hi + lo bf16 half-tiles, 4-byte words per buffer
   float *tile = reinterpret_cast<float *>(smem);                   // 2 x kTileWords
-  float *cx = tile + 2 * kTileWords;                                // 2 x 4 waves x 16 regs x 64 lanes
+  float *cx = tile + 2 * kTileWords;                                // kD x 4 waves x 16 regs x 64 lanes
+  uint32_t *sync = reinterpret_cast<uint32_t *>(cx + kD * 4 * 16 * 64 + 4 * 32 * kB * 2);
+  uint32_t *published = sync;       // [w]: tiles pair w's producer has written
+  uint32_t *consumed = sync + 4;    // [w]: tiles pair w's consumer has read
+  uint32_t *staged = sync + 8;      // producer arrivals (4 per tile)
+  uint32_t *abort = sync + 9;
   const int wave = threadIdx.x >> 6;
   const int w = wave & 3;
   const int lane = lane_id();
@@ -496,6 +529,7 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
   const uint64_t r1 = min(p.n, r0 + rows_per_chunk);
   const int ntiles = r1 > r0 ? static_cast<int>((r1 - r0 + kTile - 1) / kTile) : 0;
   const uint64_t q0 = static_cast<uint64_t>(qg) * 128 + w * 32;
+  if (threadIdx.x < 16) sync[threadIdx.x] = 0u;
 
   if (wave < 4) {
     // ---- producer ------------------------------------------------------------------------
@@ -552,54 +586,104 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
     float4 stage[kPerThread];
     load_tile(r0, stage);
     store_tile(0, stage);
-    __syncthreads();
-    for (int s = 0; s <= ntiles; ++s) {
-      if (s < ntiles) {
-        const int buf = s & 1;
-        const bool more = s + 1 < ntiles;
-        if (more) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 1), stage);
-        f32x16 c = {};
-        const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
+    __syncthreads();  // the only block-wide barrier: tile 0 staged, sync words zeroed
+    const bool diag = p.merge_count != nullptr;
+    uint64_t t_slot = 0, t_staged = 0;
+    const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
+    int slot = 0;
+    for (int s = 0; s < ntiles; ++s) {
+      const int buf = s & 1;
+      const bool more = s + 1 < ntiles;
+      if (more) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 1), stage);
+      f32x16 c = {};
+      const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
 #pragma unroll
-        for (int st = 0; st < K / 16; ++st) {
-          const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * st);
-          const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * st);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[st], bh, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c, 0, 0, 0);
-        }
-        float *out = cx + ((buf * 4 + w) * 16) * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) out[r * 64] = c[r];
-        if (more) store_tile(buf ^ 1, stage);
+      for (int st = 0; st < K / 16; ++st) {
+        const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * st);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * st);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[st], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c, 0, 0, 0);
       }
-      __syncthreads();
+      // ring slot s % kD is free once the consumer has read tile s - kD
+      const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
+      if (s >= kD && !lds_wait_ge(&consumed[w], static_cast<uint32_t>(s + 1 - kD), abort)) break;
+      if (diag) t_slot += __builtin_amdgcn_s_memtime() - tw;
+      float *out = cx + ((slot * 4 + w) * 16) * 64 + lane;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[r * 64] = c[r];
+      lds_publish(&published[w], static_cast<uint32_t>(s + 1));
+      slot = slot + 1 == kD ? 0 : slot + 1;
+      if (more) {
+        // every producer has finished this step's MFMAs on `buf` before any stages tile s + 2 into
+        // it, and tile s + 1 is complete before any reads it
+        store_tile(buf ^ 1, stage);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_fetch_add(staged, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t tb = diag ? __builtin_amdgcn_s_memtime() : 0;
+        if (!lds_wait_ge(staged, static_cast<uint32_t>(4 * (s + 1)), abort)) break;
+        if (diag) t_staged += __builtin_amdgcn_s_memtime() - tb;
+      }
+    }
+    if (diag && lane == 0) {  // diagnostics: producer rows after the consumers' (tools/flat_diag.py)
+      unsigned long long *st =
+          reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (1024 + blockIdx.x * 4 + w) * 4;
+      st[0] = __builtin_amdgcn_s_memtime() - t_start;
+      st[1] = t_slot;
+      st[2] = t_staged;
+      st[3] = 0;
     }
   } else {
     // ---- consumer ------------------------------------------------------------------------
-    float *bd = cx + 2 * 4 * 16 * 64 + w * 32 * kB * 2;  // 32 queries x kB
+    float *bd = cx + kD * 4 * 16 * 64 + w * 32 * kB * 2;  // 32 queries x kB
     uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
     Shortlists S;
     init_shortlists(p, q0, h, S);
     uint64_t t_app = 0, t_fold = 0;
     __syncthreads();
-    for (int s = 0; s <= ntiles; ++s) {
-      if (s >= 1) {
-        const int t = s - 1;
-        const uint64_t row0 = r0 + static_cast<uint64_t>(kTile) * t;
-        const uint64_t row = row0 + col;
-        const uint32_t rid = static_cast<uint32_t>(row * p.row_step);
-        bool live = row < r1;
-        const float bn = p.norms[(live ? row : r0) * p.row_step];
-        if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
-        const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
-        const float *in = cx + (((t & 1) * 4 + w) * 16) * 64 + lane;
-        f32x16 c;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) c[r] = in[r * 64];
-        tile_candidates<kB>(p, c, bn, rid, live_mask, t == ntiles - 1, S, bd, bi, t_app, t_fold);
+    const bool diag = p.merge_count != nullptr;
+    uint64_t t_wait = 0;
+    const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
+    int slot = 0;
+    bool ok = true;
+    for (int t = 0; t < ntiles; ++t) {
+      const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
+      if (!lds_wait_ge(&published[w], static_cast<uint32_t>(t + 1), abort)) {
+        ok = false;
+        break;
       }
-      __syncthreads();
+      if (diag) t_wait += __builtin_amdgcn_s_memtime() - tw;
+      const uint64_t row0 = r0 + static_cast<uint64_t>(kTile) * t;
+      const uint64_t row = row0 + col;
+      const uint32_t rid = static_cast<uint32_t>(row * p.row_step);
+      bool live = row < r1;
+      const float bn = p.norms[(live ? row : r0) * p.row_step];
+      if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
+      const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
+      const float *in = cx + ((slot * 4 + w) * 16) * 64 + lane;
+      f32x16 c;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) c[r] = in[r * 64];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's reads are done before it is released
+      lds_publish(&consumed[w], static_cast<uint32_t>(t + 1));
+      slot = slot + 1 == kD ? 0 : slot + 1;
+      tile_candidates<kB>(p, c, bn, rid, live_mask, t == ntiles - 1, S, bd, bi, t_app, t_fold);
+    }
+    if (!ok) {
+      // aborted: an unprovable shortlist (cutoff -FLT_MAX, no ids) makes the merge flag every query
+      // of the group, and the flagged queries are recomputed exhaustively
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        S.ld[r] = -FLT_MAX;
+        S.li[r] = 0xffffffffu;
+      }
+    }
+    if (diag && lane == 0) {  // diagnostics: total, appends, fold rounds, waiting for the producer
+      unsigned long long *st = reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * 4 + w) * 4;
+      st[0] = __builtin_amdgcn_s_memtime() - t_start;
+      st[1] = t_app;
+      st[2] = t_fold;
+      st[3] = t_wait;
     }
     store_shortlists(p, q0, chunk, S);
   }
@@ -1143,11 +1227,14 @@ size_t scan_lds() {
 }
 
 template <int K>
-constexpr int ws_buf() { return K >= 192 ? 64 : 80; }  // consumer buffers shrink to fit 160 KB
+constexpr int ws_buf() { return 64; }  // consumer buffers shrink to fit 160 KB
+template <int K>
+constexpr int ws_ring() { return K <= 160 ? 3 : 2; }  // contraction slots per producer/consumer pair
 
 template <int K>
 size_t ws_lds() {
-  return static_cast<size_t>(2 * kTile * (K + 8)) * 4 + 2 * 4 * 16 * 64 * 4 + 4 * (32 * ws_buf<K>() * 8);
+  return static_cast<size_t>(2 * kTile * (K + 8)) * 4 + ws_ring<K>() * 4 * 16 * 64 * 4 + 4 * (32 * ws_buf<K>() * 8) +
+         16 * 4;
 }
 
 template <int KS>
@@ -1231,11 +1318,11 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
   }
   // the warp-specialised kernel for the split contraction; the single-role kernel for the f32
   // contraction and the diagnostics (ablation, per-phase stamps)
-  const bool ws = p.split && p.ablate == 0 && p.merge_count == nullptr && std::getenv("ALAYA_FLAT_WS0") == nullptr;
+  const bool ws = p.split && p.ablate == 0 && std::getenv("ALAYA_FLAT_WS0") == nullptr;
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
     if (ws)                                                                                    \
-      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>()>), dim3(blocks), dim3(512),       \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>()>), dim3(blocks), dim3(512),       \
                          ws_lds<K>(), s, p);                                                   \
     else if (p.split)                                                                          \
       hipLaunchKernelGGL((flat_scan_kernel<K, true>), dim3(blocks), dim3(256), lds, s, p);     \

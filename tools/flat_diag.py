@@ -3,6 +3,8 @@ import os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if os.environ.get("ALAYA_AB_ROOT"):  # a saved build (e.g. ab/base)
+    sys.path.insert(0, os.environ["ALAYA_AB_ROOT"])
 import torch
 from alayalite_amd import _native
 from workloads.datasets import uniform
@@ -28,5 +30,9 @@ for ablate in (0, 1, 2, 0, 1, 2):
     m = mc.cpu().numpy()
     sm = mc[4096:].cpu().numpy().view(np.uint64).reshape(-1, 4)[:1024].astype(np.float64)
     st = sm; tot = st[:, 0].mean()
-    print(f"   per-wave memtime ticks: total {tot:.0f} append {st[:,1].mean()/tot:.2f} fold {st[:,2].mean()/tot:.2f} (max-wave {st[:,2].max()/tot:.2f}) barrier {st[:,3].mean()/tot:.2f}")
+    print(f"   per-wave memtime ticks: total {tot:.0f} append {st[:,1].mean()/tot:.2f} fold {st[:,2].mean()/tot:.2f} (max-wave {st[:,2].max()/tot:.2f}) barrier/wait {st[:,3].mean()/tot:.2f}")
+    pr = mc[4096:].cpu().numpy().view(np.uint64).reshape(-1, 4)[1024:2048].astype(np.float64)
+    if ablate == 0 and pr[:, 0].mean() > 0:  # warp-specialised scan: producer rows
+        pt = pr[:, 0].mean()
+        print(f"   producers: total {pt:.0f} wait-for-slot {pr[:,1].mean()/pt:.2f} wait-for-staging {pr[:,2].mean()/pt:.2f}")
     print(f"ablate={ablate} scan {a.elapsed_time(b):.3f} ms  merges/block mean {m[:256].mean():.1f} max {m[:256].max()}")
