@@ -291,10 +291,12 @@ def pmc_traffic(cfg):
 
     best = None
     # latest round first: on equal ef gaps the most recent profile of the kernel wins
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic*.json")), reverse=True):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
+            continue
+        if t.get("kernel", "hnsw_search_kernel") != "hnsw_search_kernel":  # flat scans: traffic_flat*.json
             continue
         c = t["config"]
         if all(c.get(k) == v for k, v in cfg.items() if k != "ef_search"):
@@ -658,8 +660,9 @@ def main():
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
     prof = pmc_traffic({"n_base": args.n, "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef})
-    if prof is not None and not use_sq8 and args.workload == "gist-hnsw":
-        # measured HBM bytes per algorithmic byte (PMC, gfx950-corrected) x this launch's bytes
+    if prof is not None and world == 1:
+        # measured HBM bytes per algorithmic byte (PMC, gfx950-corrected) of the search kernel x
+        # this launch's bytes (SQ8: the search's ratio applied to search + rerank bytes)
         traffic_bytes = prof[1]["traffic_over_algorithmic"] * bytes_launch
         traffic = {"gbs": round(traffic_bytes / (kernel_ms * 1e-3) / 1e9, 1),
                    "bytes_per_launch": int(traffic_bytes),

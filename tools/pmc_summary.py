@@ -47,11 +47,15 @@ def main(src, dst, mode="hnsw"):
         alg = 4.0 * cf["dim"] * (cf["n_base"] + cf["n_queries"]) + 4.0 * cf["n_base"]
     else:
         alg = cfg["roofline"]["algorithmic_bytes_per_launch"]
+        if cfg.get("dtype") == "u8+f32":  # SQ8: the profiled kernel is the search; the rerank's f32 rows
+            cf = cfg["config"]            # (k + 1 per query, bench.py) belong to rerank_kernel
+            alg -= 4.0 * cf["dim"] * (cf["k"] + (1 if cf["ef_search"] > cf["k"] else 0)) * cf["n_queries"]
     hit = c.get("TCC_HIT_sum", 0.0)
     miss = c.get("TCC_MISS_sum", 0.0)
     out = {
         "kernel": names.pop() if names else kernel,
-        "config": {k: cfg["config"][k] for k in ("n_base", "n_queries", "dim", "k", "ef_search") if k in cfg["config"]},
+        "config": {k: cfg["config"][k] for k in ("workload", "n_base", "n_queries", "dim", "k", "ef_search")
+                   if k in cfg["config"]},
         "launches_per_pass": launches,
         "counters_per_launch": c,
         "hbm_read_bytes_per_launch": read_b,
