@@ -193,7 +193,9 @@ int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries,
  * folded into a 128/256-entry list for k > 24) is rescored with the exact device metric
  * (l2_sqr_avx2 order) and sorted by (distance, id).  A query whose shortlist cannot be proven to
  * hold the exact top-k (error bound in flat_kernels.hip) is flagged; the host API recomputes it
- * exhaustively and reports how many it did. */
+ * exhaustively and reports how many it did.  The device variant is asynchronous on `stream` and
+ * only writes d_flags[q] = 1 for such a query (its d_ids row is then not proven exact): the caller
+ * recomputes it, e.g. through alaya_index_flat_search. */
 int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
                             uint32_t *ids, float *dists, uint32_t *n_recomputed);
 int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
