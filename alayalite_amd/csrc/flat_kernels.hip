@@ -1232,10 +1232,19 @@ template <int K>
 constexpr int ws_ring() { return K <= 160 ? 3 : 2; }  // contraction slots per producer/consumer pair
 
 template <int K>
-size_t ws_lds() {
+constexpr size_t ws_lds() {
   return static_cast<size_t>(2 * kTile * (K + 8)) * 4 + ws_ring<K>() * 4 * 16 * 64 * 4 + 4 * (32 * ws_buf<K>() * 8) +
          16 * 4;
 }
+// every narrow-row instantiation fits one block's 160 KB of LDS, and a candidate buffer holds a
+// whole tile of appends on top of the 32 a due fold leaves (tile_candidates' `need` rule)
+template <int K>
+constexpr bool ws_fits() {
+  return ws_lds<K>() <= 160 * 1024 && ws_buf<K>() >= 2 * kTile;
+}
+static_assert(ws_fits<32>() && ws_fits<64>() && ws_fits<96>() && ws_fits<128>() && ws_fits<160>() &&
+                  ws_fits<192>() && ws_fits<224>(),
+              "warp-specialised scan: LDS ring / candidate buffers");
 
 template <int KS>
 size_t wide_lds() {
