@@ -213,10 +213,17 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     // Several queries per resident slot: residency beyond what keeps a table of ~32 ef slots
     // (load <= ~0.5 at the usual 10-24 ef visited ids) costs more in probes and spills than it
     // gains (SIFT 1M, 10k queries: 4 waves/SIMD with 8 KB tables beat 5 with 4 KB by ~20 %).
-    const uint32_t tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(32ull * ef)));
-    const bool tc = mode != 2 && fits_compact(tl);
-    const size_t per_block = fixed + (static_cast<size_t>(tc ? 2 : 4) << tl);
-    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kLdsPerCu / per_block));
+    uint32_t tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(32ull * ef)));
+    auto per_block = [&](uint32_t l) {
+      const bool tc = mode != 2 && fits_compact(l);
+      return fixed + (static_cast<size_t>(tc ? 2 : 4) << l);
+    };
+    // ... but never leave a SIMD without a wave for it: halve the table (down to ~16 ef slots)
+    // while fewer than one block per SIMD would fit (10M x 768 SQ8 at ef 340: 32 KB tables admit
+    // 3 of the 4 waves the register file allows)
+    const uint64_t simd_floor = std::min<uint64_t>(4, static_cast<uint64_t>(vgpr_blocks));
+    while (kLdsPerCu / per_block(tl) < simd_floor && tl > 10 && (1ull << (tl - 1)) >= 16ull * ef) --tl;
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kLdsPerCu / per_block(tl)));
   }
   const size_t budget = kLdsPerCu / blocks > fixed ? kLdsPerCu / blocks - fixed : 0;
   auto pick = [&](size_t slot_bytes, uint32_t lmax) {
