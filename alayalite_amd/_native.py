@@ -12,7 +12,25 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def _runtime_order():
+    """PyTorch-ROCm bundles its own HIP + HSA runtime (torch/lib) beside /opt/rocm's, which this
+    engine links.  Both live in one process only in one order: torch's runtime loaded and
+    initialised first, then the engine's.  Loading the engine first left the engine with no device
+    ("no HIP device available") once torch initialised afterwards (a GPU test run, r03), and
+    initialising the engine first leaves torch without devices.  So when torch is importable it is
+    loaded and initialised here, before the extension."""
+    try:
+        import torch
+    except ImportError:  # the engine itself does not need torch
+        return
+    try:
+        torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        pass
+
+
 def _load():
+    _runtime_order()
     try:
         return importlib.import_module("alayalite_amd._alayalitepy")
     except ImportError as exc:  # pragma: no cover - exercised only on a broken install

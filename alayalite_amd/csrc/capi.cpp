@@ -334,6 +334,9 @@ void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStr
   const char *env = std::getenv("ALAYA_FLAT_PRESCAN");
   const uint64_t step = env ? std::strtoull(env, nullptr, 10) : 0;
   if (step < 2 || p.n / step < 1024) return;
+  // the slabbed wide scan (rows past 224 floats) reads contiguous rows and has no row_step: its
+  // "sample" would be the first n/S rows, so the prescan is off there
+  if (alaya_amd::flat_query_width(ix->stride) != 0) return;
   alaya_amd::FlatParams q = p;
   q.n = (p.n + step - 1) / step;
   q.row_step = static_cast<uint32_t>(step);
@@ -388,6 +391,8 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
   const int chunks = flat_chunks(ix, nqg, ix->n);
   p.n_chunks = chunks;
   p.row_step = 1;
+  const char *spin = std::getenv("ALAYA_FLAT_SPIN_LIMIT");  // debug override (tests force an abort)
+  p.spin_limit = spin ? static_cast<uint32_t>(std::strtoul(spin, nullptr, 10)) : (1u << 20);
   const size_t cand = static_cast<size_t>(chunks) * nq * alaya_amd::flat_shortlist();
   ix->cand_d.reserve(cand * 4);
   ix->cand_i.reserve(cand * 4);
@@ -551,7 +556,7 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     set_device(ix);
     scratch_drain(ix);
     const uint32_t stride = round_up32(dim);
-    if (ix->has_sq8 && (n != ix->n || dim != ix->dim)) {  // the codes no longer describe these rows
+    if (ix->has_sq8) {  // new rows: the codes describe the old ones, whatever the shape
       ix->has_sq8 = false;
       ix->codes.release();
       ix->sq_min.release();
@@ -678,7 +683,11 @@ void reserve_locked(alaya_index *ix, uint64_t capacity) {
   ix->capacity = std::max(ix->capacity, capacity);
 }
 
+// The three patch helpers below change buffers an in-flight search reads (rows, adjacency, the
+// validity bitmap), so each first waits for every earlier launch on the index (alaya_hip.h's
+// stream contract: a call is ordered after the launches before it).
 void write_rows_locked(alaya_index *ix, uint64_t first, const float *rows, uint64_t count) {
+  scratch_drain(ix);
   const size_t row = static_cast<size_t>(ix->stride) * 4;
   if (first + count > ix->capacity || (first + count) * row > ix->base.bytes)
     throw ArgError("rows beyond the reserved capacity");
@@ -693,6 +702,7 @@ void write_rows_locked(alaya_index *ix, uint64_t first, const float *rows, uint6
 
 void write_edges_locked(alaya_index *ix, const uint32_t *ids, const uint32_t *edges, uint64_t count) {
   if (!ix->has_graph) throw ArgError("index has no graph");
+  scratch_drain(ix);
   for (uint64_t i = 0; i < count; ++i) {
     if (ids[i] >= ix->capacity || ids[i] >= ix->n || (static_cast<uint64_t>(ids[i]) + 1) * ix->R * 4 > ix->l0.bytes ||
         (ix->has_overlay && (static_cast<uint64_t>(ids[i]) + 1) * 4 > ix->levels.bytes))
@@ -712,6 +722,7 @@ void write_edges_locked(alaya_index *ix, const uint32_t *ids, const uint32_t *ed
 void set_valid_locked(alaya_index *ix, uint64_t id, bool valid) {
   if (!ix->has_valid || id >= ix->capacity || (id / 32 + 1) * 4 > ix->valid.bytes)
     throw ArgError("id out of range (reserve capacity first)");
+  scratch_drain(ix);
   uint32_t w = 0;
   uint32_t *dw = ix->valid.as<uint32_t>() + (id >> 5);
   hip_check(hipMemcpy(&w, dw, 4, hipMemcpyDeviceToHost), "read bitmap");
@@ -1300,25 +1311,39 @@ int alaya_index_set_sq8(alaya_index *ix, const uint8_t *codes, uint64_t n, uint3
 
 // SQ8 graph search (+ optional rerank) on device buffers.  The search writes its ks = k (reference
 // rerank) or ef (corrected rerank) ids into ix->sq_ids; the rerank reads them and writes d_ids.
+// shard >= 0: shard mode (alaya_index_shard_search_sq8_device) with the reference rerank, the id-0
+// zero entries only when shard == 1 (this shard holds global row 0), empty slots (kEmpty, FLT_MAX).
 static void sq8_search_dev(alaya_index *ix, const float *d_q, const float *d_rq, uint64_t nq, uint32_t k,
                            uint32_t ef, int rerank, uint32_t *d_ids, float *d_dists, uint32_t *d_cnt,
-                           hipStream_t s) {
+                           hipStream_t s, int shard = -1) {
   if (rerank < 0 || rerank > 2) throw ArgError("rerank must be 0 (none), 1 (reference) or 2 (corrected)");
   if (nq == 0 || k == 0) return;
   if (!rerank) {
-    do_search(ix, d_q, nq, k, ef, d_ids, d_dists, d_cnt, s, nullptr, true);
+    do_search(ix, d_q, nq, k, ef, d_ids, d_dists, d_cnt, s, nullptr, true, shard >= 0 ? 0xffffffffu : 0u);
     return;
   }
-  const uint32_t ks = rerank == 2 ? ef : k;  // corrected: the whole ef pool, kEmpty past the pool
+  const bool corrected = rerank == 2;
+  const uint32_t ks = corrected ? ef : k;  // corrected: the whole ef pool, kEmpty past the pool
   ix->sq_ids.reserve(nq * ks * 4);
   ix->sq_d.reserve(nq * ks * 4);
+  // search fill: the reference's zero-initialised pool slots (rescored as row 0) on a single index
+  // and on the shard holding global row 0; empty elsewhere (skipped by the rerank)
+  const uint32_t search_fill = (corrected || shard == 0) ? 0xffffffffu : 0u;
   do_search(ix, d_q, nq, ks, ef, ix->sq_ids.as<uint32_t>(), ix->sq_d.as<float>(), d_cnt, s, nullptr, true,
-            rerank == 2 ? 0xffffffffu : 0u);
+            search_fill);
   SearchParams p = base_params(ix);
   p.queries = d_rq ? d_rq : d_q;
   p.nq = nq;
   p.q_stride = ix->dim;
-  alaya_amd::RerankParams r{ix->sq_ids.as<uint32_t>(), k, ef, ks, rerank == 2 ? 1 : 0, d_ids, d_dists};
+  alaya_amd::RerankParams r{};
+  r.search_ids = ix->sq_ids.as<uint32_t>();
+  r.k = k;
+  r.n_src = ks;
+  r.n_take = corrected ? ef : std::min(k, ef);
+  r.zeros = (!corrected && shard != 0 && ef > k) ? ef - k : 0u;
+  r.fill_id = shard >= 0 ? 0xffffffffu : 0u;
+  r.out_ids = d_ids;
+  r.out_dists = d_dists;
   hip_check(alaya_amd::launch_rerank(p, r, s), "rerank launch");
   scratch_release(ix, s);  // the rerank read the search's ids from the index's sq_ids buffer
 }
@@ -1362,6 +1387,18 @@ int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries,
     set_device(ix);
     sq8_search_dev(ix, d_queries, d_rerank_queries, nq, k, ef, rerank, d_ids, d_dists, d_counters,
                    static_cast<hipStream_t>(stream));
+  });
+}
+
+int alaya_index_shard_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
+                                        uint64_t nq, uint32_t k, uint32_t ef, int holds_row0, uint32_t *d_ids,
+                                        float *d_dists, uint32_t *d_counters, void *stream) {
+  return guarded([&] {
+    if (!ix || (nq && (!d_queries || !d_ids || !d_dists))) throw ArgError("invalid arguments");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    set_device(ix);
+    sq8_search_dev(ix, d_queries, d_rerank_queries, nq, k, ef, 1, d_ids, d_dists, d_counters,
+                   static_cast<hipStream_t>(stream), holds_row0 ? 1 : 0);
   });
 }
 

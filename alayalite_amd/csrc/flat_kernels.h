@@ -34,6 +34,8 @@ struct FlatParams {
   int split;           // 1 = bf16 hi/lo split contraction (3 bf16 MFMAs), 0 = f32 MFMA
   int ablate;          // diagnostics only: 1 = skip candidate handling (MFMA + tile stream only)
   uint32_t *merge_count;  // diagnostics only (nullable): merges per block
+  uint32_t spin_limit; // warp-specialised scan: LDS-flag polls before a block aborts (its queries are
+                       // then flagged for the exhaustive redo); 1 << 20 unless ALAYA_FLAT_SPIN_LIMIT
 };
 
 int flat_shortlist();

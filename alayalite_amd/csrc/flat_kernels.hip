@@ -477,16 +477,16 @@ __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
 // draws a fold round falls up to kD - 1 tiles behind its producer instead of stalling all eight
 // waves at a barrier (the fold rounds of the four consumers fall on different tiles).
 // --------------------------------------------------------------------------------------------
-constexpr uint32_t kSpinLimit = 1u << 20;  // ~0.1 s of polling: a protocol error ends the scan, not the GPU
-
-// Wait until *a >= v (wave-uniform).  False when the block aborted (a wait ran past kSpinLimit):
+// Default poll limit (p.spin_limit): ~0.1 s of polling, so a protocol error ends the scan, not the
+// GPU.  ALAYA_FLAT_SPIN_LIMIT overrides it (tests force aborts with a tiny limit).
+// Wait until *a >= v (wave-uniform).  False when the block aborted (a wait ran past the limit):
 // every later wait then returns at once, the loops end and the shortlists are written as
 // unprovable (see flat_scan_ws_kernel), so the merge flags the queries for the exhaustive redo.
-__device__ __forceinline__ bool lds_wait_ge(uint32_t *a, uint32_t v, uint32_t *abort) {
+__device__ __forceinline__ bool lds_wait_ge(uint32_t *a, uint32_t v, uint32_t *abort, uint32_t limit) {
   for (uint32_t n = 0;; ++n) {
     if (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) break;
     if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) return false;
-    if (n == kSpinLimit) {
+    if (n >= limit) {
       if (__lane_id() == 0) __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return false;
     }
@@ -607,7 +607,7 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
       }
       // ring slot s % kD is free once the consumer has read tile s - kD
       const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-      if (s >= kD && !lds_wait_ge(&consumed[w], static_cast<uint32_t>(s + 1 - kD), abort)) break;
+      if (s >= kD && !lds_wait_ge(&consumed[w], static_cast<uint32_t>(s + 1 - kD), abort, p.spin_limit)) break;
       if (diag) t_slot += __builtin_amdgcn_s_memtime() - tw;
       float *out = cx + ((slot * 4 + w) * 16) * 64 + lane;
 #pragma unroll
@@ -621,7 +621,7 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         if (lane == 0) __hip_atomic_fetch_add(staged, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint64_t tb = diag ? __builtin_amdgcn_s_memtime() : 0;
-        if (!lds_wait_ge(staged, static_cast<uint32_t>(4 * (s + 1)), abort)) break;
+        if (!lds_wait_ge(staged, static_cast<uint32_t>(4 * (s + 1)), abort, p.spin_limit)) break;
         if (diag) t_staged += __builtin_amdgcn_s_memtime() - tb;
       }
     }
@@ -648,7 +648,7 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
     bool ok = true;
     for (int t = 0; t < ntiles; ++t) {
       const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-      if (!lds_wait_ge(&published[w], static_cast<uint32_t>(t + 1), abort)) {
+      if (!lds_wait_ge(&published[w], static_cast<uint32_t>(t + 1), abort, p.spin_limit)) {
         ok = false;
         break;
       }

@@ -811,6 +811,14 @@ class DeviceIndex {
                                               reinterpret_cast<uint32_t *>(counters),
                                               reinterpret_cast<void *>(stream)));
   }
+  void shard_search_sq8_device(uintptr_t q, uintptr_t rq, uint64_t nq, uint32_t k, uint32_t ef, bool holds_row0,
+                               uintptr_t ids, uintptr_t dists, uintptr_t counters, uintptr_t stream) {
+    check(alaya_index_shard_search_sq8_device(ix_, reinterpret_cast<const float *>(q),
+                                              reinterpret_cast<const float *>(rq), nq, k, ef, holds_row0 ? 1 : 0,
+                                              reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
+                                              reinterpret_cast<uint32_t *>(counters),
+                                              reinterpret_cast<void *>(stream)));
+  }
   py::tuple flat_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k) {
     const uint64_t nq = q.shape(0);
     py::array_t<uint32_t> ids({static_cast<py::ssize_t>(nq), static_cast<py::ssize_t>(k)});
@@ -960,6 +968,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("flat_search_device", &DeviceIndex::flat_search_device)
       .def("flat_diag", &DeviceIndex::flat_diag)
       .def("search_sq8_device", &DeviceIndex::search_sq8_device)
+      .def("shard_search_sq8_device", &DeviceIndex::shard_search_sq8_device)
       .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)
       .def("search_sq8", &DeviceIndex::search_sq8, py::arg("queries"), py::arg("k"), py::arg("ef"),
            py::arg("rerank") = 1, py::arg("rerank_queries") = py::none())

@@ -59,12 +59,21 @@ struct SearchParams {
   const float *sq_max;
 };
 
-// PyIndex::rerank inputs (python/include/index.hpp:450-488).
+// PyIndex::rerank inputs (python/include/index.hpp:450-488).  Per query the kernel rescores
+// search_ids[0 .. n_take) (row stride n_src; kEmpty entries are skipped) plus `zeros` entries of id 0
+// -- the reference's res_pool slots [k, ef) that batch_search leaves zero (index.hpp:301) -- and
+// returns the k smallest pair<dist, id>.
+//   reference mode:  n_take = min(k, ef), zeros = ef - k, fill_id = 0
+//   corrected mode:  n_take = ef (the whole pool, kEmpty past it), zeros = 0, fill_id = 0
+//   shard mode:      n_take = min(k, ef); zeros = ef - k only on the shard that holds global row 0,
+//                    else 0; fill_id = kEmpty (see alaya_index_shard_search_sq8_device)
 struct RerankParams {
   const uint32_t *search_ids;  // nq x n_src ids written by the SQ8 search
-  uint32_t k, ef;
-  uint32_t n_src;              // ids per query in search_ids (k, or ef in corrected mode)
-  int corrected;               // 0: reference (ef-k zero entries rescored), 1: the ef pool entries
+  uint32_t k;
+  uint32_t n_src;              // ids per query row of search_ids
+  uint32_t n_take;             // ids rescored per query (<= n_src)
+  uint32_t zeros;              // multiplicity of the extra id-0 entry (0 = none)
+  uint32_t fill_id;            // output slots without a candidate: 0 -> (0, 0.0), kEmpty -> (kEmpty, FLT_MAX)
   uint32_t *out_ids;           // nq x k
   float *out_dists;            // nq x k (nullable)
 };

@@ -346,9 +346,11 @@ __global__ void __launch_bounds__(64) row_distance_kernel(SearchParams p, const 
 // PyIndex::rerank (python/include/index.hpp:450-488) for SQ8 indexes, Linux batch path (:337-345):
 // res_pool[i] holds the k ids the search wrote plus ef-k zeros; all ef entries are rescored with
 // the raw-space QueryComputer (f32 rows, FLT_MAX for invalid rows) and the k smallest
-// pair<dist, id> are returned (id 0 can repeat -- reference behaviour).  Corrected mode (SURVEY
-// A12 "corrected mode behind a flag"): the search hands over its whole ef pool (slots past the pool
-// hold kEmpty and are skipped), so every rescored entry is a real candidate.  One wave per query.
+// pair<dist, id> are returned (id 0 can repeat -- reference behaviour).  The ef-k zero entries
+// are one rescored entry of multiplicity rp.zeros.  Corrected mode (SURVEY A12 "corrected mode
+// behind a flag") hands over the whole ef pool with no zeros; shard mode keeps the zeros only on
+// the shard holding global row 0 (RerankParams).  kEmpty ids (slots past a pool) are skipped.
+// One wave per query.
 template <bool kIP>
 __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams rp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -358,9 +360,10 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
   float *cd = reinterpret_cast<float *>(cid + cap);
   uint32_t *cm = reinterpret_cast<uint32_t *>(cd + cap);
   const int lane = lane_id();
-  const uint32_t taken = rp.corrected ? rp.n_src : min(rp.k, rp.ef);
-  const uint32_t zeros = (!rp.corrected && rp.ef > rp.k) ? rp.ef - rp.k : 0u;
+  const uint32_t taken = rp.n_take;
+  const uint32_t zeros = rp.zeros;
   const uint32_t c = taken + (zeros ? 1u : 0u);
+  const float fill_d = rp.fill_id == kEmpty ? FLT_MAX : 0.f;
   for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
     const float *qsrc = p.queries + qi * p.q_stride;
     for (uint32_t e = lane; e < p.stride; e += 64) q[e] = e < p.dim ? qsrc[e] : 0.f;
@@ -371,7 +374,7 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
       if (i < c) {
         id = i < taken ? rp.search_ids[qi * rp.n_src + i] : 0u;
         m = i < taken ? 1u : zeros;
-        if (id == kEmpty) {  // corrected mode: slot past the pool
+        if (id == kEmpty) {  // a slot past the pool
           id = 0u;
           m = 0u;
         }
@@ -401,8 +404,8 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
       }
     }
     for (uint32_t i = nv + lane; i < rp.k; i += 64) {  // fewer candidates than k
-      rp.out_ids[qi * rp.k + i] = 0u;
-      if (rp.out_dists) rp.out_dists[qi * rp.k + i] = 0.f;
+      rp.out_ids[qi * rp.k + i] = rp.fill_id;
+      if (rp.out_dists) rp.out_dists[qi * rp.k + i] = fill_d;
     }
     wave_sync();
   }

@@ -94,24 +94,162 @@ def merge_reference(ids_per_shard, dists_per_shard, offsets, k):
     return out_i, out_d
 
 
+def shard_search(index, lo: int, sq8: bool, q_dev, k: int, ef: int, ids_dev, dists_dev, counters_dev, stream,
+                 rq_dev=None):
+    """One shard's search of a device query batch into device buffers (asynchronous on `stream`, a
+    hipStream_t handle); result slots without a candidate are (0xffffffff, FLT_MAX).  SQ8 shards run
+    the SQ8 graph search plus PyIndex::rerank (index.hpp:337-345, 450-488); the reference's id-0
+    entries belong to global row 0, i.e. to the shard with lo == 0 (rq_dev: the rerank queries,
+    None = q_dev)."""
+    nq = q_dev.shape[0]
+    if sq8:
+        index.shard_search_sq8_device(q_dev.data_ptr(), 0 if rq_dev is None else rq_dev.data_ptr(), nq, k, ef,
+                                      lo == 0, ids_dev.data_ptr(), dists_dev.data_ptr(), counters_dev.data_ptr(),
+                                      stream)
+    else:
+        index.shard_search_device(q_dev.data_ptr(), nq, k, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
+                                  counters_dev.data_ptr(), stream)
+
+
+class ShardPipeline:
+    """Double-buffered query batches (overlap the exchange with the next batch's search).
+
+    Batch i's search runs on the compute stream into buffer slot i % 2; its exchange (pack, one
+    all_gather, the merge sort) runs on a second stream once the search's event fires, while the
+    compute stream already searches batch i + 1.  The search of batch i + 2 reuses slot i % 2 only
+    after batch i's exchange has read it (an event the compute stream waits on).  The host issues
+    search i + 1 before exchange i, so a blocking exchange (gloo with host copies) still overlaps the
+    device search.  On CPU tensors (gloo tests) the same loop runs without streams.
+
+    search_fn(q, ids, dists, counters, stream_handle) launches one shard search (shard_search);
+    batches hold at most nq queries each."""
+
+    def __init__(self, search_fn, nq: int, k: int, offset: int, device, group=None, timing: bool = False):
+        import torch
+
+        self.search_fn, self.k, self.offset, self.group = search_fn, k, offset, group
+        self.device = torch.device(device)
+        mk = lambda dt, w: torch.empty((nq, w), dtype=dt, device=self.device)  # noqa: E731
+        self.bufs = [(mk(torch.int32, k), mk(torch.float32, k), mk(torch.int32, 4)) for _ in range(2)]
+        self.rows = [0, 0]
+        self.gpu = self.device.type == "cuda"
+        if self.gpu:
+            self.compute = torch.cuda.Stream(self.device)
+            self.exch = torch.cuda.Stream(self.device)
+            self.searched = [torch.cuda.Event() for _ in range(2)]
+            self.exchanged = [torch.cuda.Event() for _ in range(2)]
+            self.used = [False, False]
+        self.timing = timing and self.gpu
+        self.spans = []  # (start, end) events around each search on the compute stream (timing=True)
+
+    def _slot(self, slot, m):
+        """Buffers of slot for a batch of m <= nq queries (leading rows: contiguous views)."""
+        return tuple(b[:m] for b in self.bufs[slot])
+
+    def _launch(self, q, slot):
+        ids, d, c = self._slot(slot, q.shape[0])
+        self.rows[slot] = q.shape[0]
+        if not self.gpu:
+            self.search_fn(q, ids, d, c, 0)
+            return
+        if self.used[slot]:
+            self.compute.wait_event(self.exchanged[slot])
+        if self.timing:
+            import torch
+
+            span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            span[0].record(self.compute)
+        self.search_fn(q, ids, d, c, self.compute.cuda_stream)
+        if self.timing:
+            span[1].record(self.compute)
+            self.spans.append(span)
+        self.searched[slot].record(self.compute)
+        self.used[slot] = True
+
+    def _exchange(self, slot):
+        import torch
+
+        ids, d, _ = self._slot(slot, self.rows[slot])
+        if not self.gpu:
+            return exchange_and_merge(ids, d, self.offset, self.k, self.group)
+        with torch.cuda.stream(self.exch):
+            self.exch.wait_event(self.searched[slot])
+            out = exchange_and_merge(ids, d, self.offset, self.k, self.group)
+            self.exchanged[slot].record(self.exch)
+        return out
+
+    def run(self, batches):
+        """Search + exchange every batch (device query tensors); returns the merged (ids, dists) per
+        batch, produced on the exchange stream (synchronise before reading them on the host)."""
+        out = [None] * len(batches)
+        if not batches:
+            return out
+        if self.gpu:  # the batches were produced on the caller's stream
+            import torch
+
+            self.compute.wait_stream(torch.cuda.current_stream(self.device))
+        self._launch(batches[0], 0)
+        for i in range(len(batches)):
+            if i + 1 < len(batches):
+                self._launch(batches[i + 1], (i + 1) % 2)
+            out[i] = self._exchange(i % 2)
+        if self.gpu:  # later work on the caller's stream sees the merged results
+            import torch
+
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(self.exch)
+            for ids, d in out:  # allocated on the exchange stream, used on the caller's
+                ids.record_stream(cur)
+                d.record_stream(cur)
+        return out
+
+    def search_ms(self):
+        """Mean search time (ms) of the batches run with timing=True, as the compute stream saw it
+        inside the pipeline (after synchronisation)."""
+        return float(np.mean([a.elapsed_time(b) for a, b in self.spans])) if self.spans else None
+
+    def run_sync(self, batches):
+        """The same batches without overlap: search, then exchange, one after the other on the
+        caller's current stream (the synchronous reference for the overlapped timing)."""
+        import torch
+
+        out = []
+        for q in batches:
+            ids, d, c = self._slot(0, q.shape[0])
+            stream = torch.cuda.current_stream(self.device).cuda_stream if self.gpu else 0
+            self.search_fn(q, ids, d, c, stream)
+            out.append(exchange_and_merge(ids, d, self.offset, self.k, self.group))
+        return out
+
+
 class ShardedIndex:
-    """This rank's shard on its GPU: rows [lo, hi) of `base`, graph built on the shard."""
+    """This rank's shard on its GPU: rows [lo, hi) of `base`, graph built on the shard.  sq8=True
+    adds the shard's SQ8 space (SQ8Space::fit on the shard's rows, sq8_space.hpp:116-127): searches
+    then run on the codes and rerank on the f32 rows (config 5)."""
 
     def __init__(self, base, world: int, rank: int, device: int = 0, metric: int = 0, R: int = 32,
-                 ef_construction: int = 100, num_threads: int = 1, graph=None):
+                 ef_construction: int = 100, num_threads: int = 1, graph=None, sq8: bool = False):
         from ._native import _ext
 
         self.lo, self.hi = shard_range(base.shape[0], world, rank)
         self.rows = np.ascontiguousarray(base[self.lo:self.hi])
         self.graph = graph if graph is not None else _ext.Graph.build(self.rows, metric, R, ef_construction, num_threads, 100)
+        self._device = device
         self.index = _ext.DeviceIndex(device)
         self.index.set_base(self.rows, metric)
         self.index.set_graph(self.graph)
+        self.sq8 = None
+        if sq8:
+            mn, mx = _ext.sq8_train(self.rows)
+            order = _ext.host_sq8_order()
+            codes = _ext.sq8_encode(self.rows, mn, mx, max(1, num_threads))
+            self.index.set_sq8(codes, mn, mx, order)
+            self.sq8 = (codes, mn, mx, order)
 
-    def search_device(self, q_dev, k: int, ef: int, ids_dev, dists_dev, counters_dev, stream):
-        """This shard's search; result slots past the pool are (0xffffffff, FLT_MAX)."""
-        self.index.shard_search_device(q_dev.data_ptr(), q_dev.shape[0], k, ef, ids_dev.data_ptr(),
-                                       dists_dev.data_ptr(), counters_dev.data_ptr(), stream)
+    def search_device(self, q_dev, k: int, ef: int, ids_dev, dists_dev, counters_dev, stream, rq_dev=None):
+        """This shard's search; result slots without a candidate are (0xffffffff, FLT_MAX)."""
+        shard_search(self.index, self.lo, self.sq8 is not None, q_dev, k, ef, ids_dev, dists_dev, counters_dev,
+                     stream, rq_dev)
 
     def search(self, q_dev, k: int, ef: int, stream, group=None):
         import torch
@@ -122,3 +260,13 @@ class ShardedIndex:
         c = torch.empty((nq, 4), dtype=torch.int32, device=q_dev.device)
         self.search_device(q_dev, k, ef, ids, d, c, stream)
         return exchange_and_merge(ids, d, self.lo, k, group)
+
+    def pipeline(self, nq: int, k: int, ef: int, group=None) -> ShardPipeline:
+        """A double-buffered pipeline for batches of nq queries at this ef (ShardPipeline)."""
+        fn = lambda q, ids, d, c, s: self.search_device(q, k, ef, ids, d, c, s)  # noqa: E731
+        return ShardPipeline(fn, nq, k, self.lo, self.index_device(), group)
+
+    def index_device(self):
+        import torch
+
+        return torch.device("cuda", self._device)

@@ -485,7 +485,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from alayalite_amd import _native
-    from alayalite_amd.sharded import exchange_and_merge, shard_range
+    from alayalite_amd.sharded import exchange_and_merge, shard_range, shard_search
     import workloads.datasets as datasets
 
     native = _native._ext
@@ -532,22 +532,24 @@ def main():
     cnt_dev = torch.empty((nq, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    shard_mode = world > 1 and args.mode == "shard"
+
     def launch(ef, ix=None):
         ix = index if ix is None else ix
-        if use_sq8:  # SQ8 graph search + PyIndex::rerank as batch_search runs it (rerank mode 1)
+        if shard_mode and ix is index:
+            # per-shard search (SQ8: search + rerank, id-0 entries on the shard holding global row 0);
+            # slots without a candidate are (0xffffffff, FLT_MAX), never a spurious hit
+            shard_search(ix, lo, use_sq8, q_dev, K, ef, ids_dev, dists_dev, cnt_dev, stream.cuda_stream)
+        elif use_sq8:  # SQ8 graph search + PyIndex::rerank as batch_search runs it (rerank mode 1)
             ix.search_sq8_device(q_dev.data_ptr(), 0, nq, K, ef, 1, ids_dev.data_ptr(), dists_dev.data_ptr(),
                                  cnt_dev.data_ptr(), stream.cuda_stream)
-        elif world > 1 and args.mode == "shard" and ix is index:
-            # per-shard search: slots past the pool are (0xffffffff, FLT_MAX), never a spurious hit
-            ix.shard_search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
-                                   cnt_dev.data_ptr(), stream.cuda_stream)
         else:
             ix.search_device(q_dev.data_ptr(), nq, K, ef, ids_dev.data_ptr(), dists_dev.data_ptr(),
                              cnt_dev.data_ptr(), stream.cuda_stream)
 
     def step(ef):
         launch(ef)
-        if world > 1 and args.mode == "shard":
+        if shard_mode:
             return exchange_and_merge(ids_dev, dists_dev, lo, K)
         return ids_dev, dists_dev
 
@@ -597,7 +599,7 @@ def main():
             ev[i][0].record(stream)
             launch(ef_t)
             ev[i][1].record(stream)
-            if world > 1 and args.mode == "shard":
+            if shard_mode:
                 # exchange + merge of the same step (the search above is the per-shard kernel)
                 exchange_and_merge(ids_dev, dists_dev, lo, K)
         torch.cuda.synchronize()
@@ -622,6 +624,22 @@ def main():
 
     # ---- timed region ------------------------------------------------------------------------
     elapsed, kernel_ms = timed(ef, args.steps, args.warmup)
+    overlap = None
+    if shard_mode:
+        # the same K steps double-buffered (ShardPipeline: the search of step i+1 runs beside the
+        # all_gather + merge of step i on a second stream); this is `value`, the synchronous loop
+        # above (search, then exchange, per step) is reported beside it with the exchange alone
+        sync_elapsed = elapsed
+        elapsed, pipe_search_ms = timed_pipeline(torch, dist, dev, ef, args.steps, args.warmup, index, lo, use_sq8,
+                                                 q_dev, nq)
+        exch_ms = timed_exchange(torch, dist, ids_dev, dists_dev, lo, args.steps)
+        overlap = {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                   "sync_ms_per_step": round(sync_elapsed / args.steps * 1e3, 4),
+                   "search_ms": round(kernel_ms, 4), "search_ms_in_pipeline": round(pipe_search_ms, 4),
+                   "exchange_ms": round(exch_ms, 4),
+                   "bound_ms": round(max(pipe_search_ms, exch_ms), 4),
+                   "note": "value = the overlapped steps; sync = search then exchange in one stream per step"}
+        log("overlap", overlap)
 
     # ---- PCIe-inclusive rate (reported beside value, never value): the host-buffer API's work --
     # queries H2D from pinned host memory, the search, ids + distances D2H, each step synchronised
@@ -725,11 +743,57 @@ def main():
             out["config"]["qps_curve"] = curve
         if replica is not None:
             out["replica"] = replica
+        if overlap is not None:
+            out["exchange_overlap"] = overlap
         if pcie is not None:
             out["pcie_inclusive"] = pcie
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_dev, nq):
+    """K shard steps through ShardPipeline (double-buffered: the search of step i+1 overlaps the
+    exchange of step i); barrier + synchronize on both sides, max over ranks.  Returns (seconds,
+    mean search ms inside the pipeline, from a second untimed pass with events)."""
+    from alayalite_amd.sharded import ShardPipeline, shard_search
+
+    fn = lambda q, i, d, c, s: shard_search(index, lo, use_sq8, q, K, ef, i, d, c, s)  # noqa: E731
+    pipe = ShardPipeline(fn, nq, K, lo, dev)
+    pipe.run([q_dev] * max(1, warmup))
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pipe.run([q_dev] * steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    # the search time as it runs inside the pipeline (a separate, untimed pass with events)
+    tp = ShardPipeline(fn, nq, K, lo, dev, timing=True)
+    tp.run([q_dev] * steps)
+    torch.cuda.synchronize()
+    sm = torch.tensor([tp.search_ms()], device=dev, dtype=torch.float64)
+    dist.all_reduce(sm, op=dist.ReduceOp.MAX)
+    return el.item(), sm.item()
+
+
+def timed_exchange(torch, dist, ids_dev, dists_dev, lo, steps):
+    """The exchange alone (pack, all_gather, merge sort) on resident shard results: ms per step,
+    max over ranks."""
+    from alayalite_amd.sharded import exchange_and_merge
+
+    exchange_and_merge(ids_dev, dists_dev, lo, K)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        exchange_and_merge(ids_dev, dists_dev, lo, K)
+    torch.cuda.synchronize()
+    el = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], device=ids_dev.device, dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return el.item()
 
 
 def replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, launch, rank, world, nq,

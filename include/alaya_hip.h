@@ -184,6 +184,17 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
 int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
                                         uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *d_ids,
                                         float *d_dists, uint32_t *d_counters, void *stream);
+/* The per-shard search of a base-range sharded SQ8 index (no reference
+ * counterpart): the SQ8 graph search plus PyIndex::rerank (index.hpp:337-345, 450-488) on this
+ * shard's rows.  The reference's id-0 quirk (the ef - k zero-filled res_pool slots, :301, rescored
+ * as row 0) belongs to global row 0 only: with holds_row0 != 0 (the shard whose local row 0 is
+ * global row 0) the rerank is exactly alaya_index_batch_search_sq8_device's rerank = 1; otherwise
+ * only the k search ids are rescored.  Result slots without a candidate hold (0xffffffff, FLT_MAX),
+ * so they sort after every real candidate in the cross-shard merge.  With one shard the merged
+ * result equals the reference's batch_search.  d_dists is required. */
+int alaya_index_shard_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
+                                        uint64_t nq, uint32_t k, uint32_t ef, int holds_row0, uint32_t *d_ids,
+                                        float *d_dists, uint32_t *d_counters, void *stream);
 /* ---- flat (exhaustive) exact k-NN, L2, any dim, 1 <= k <= 224 -----------------------------------
  * No reference implementation (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); the
  * analogue is find_exact_gt (include/utils/evaluate.hpp:29-62).  An MFMA pass ranks every row

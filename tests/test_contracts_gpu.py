@@ -110,6 +110,22 @@ def test_new_base_invalidates_sq8_codes(native):
         dev.search_sq8(bigger[:2], 10, 20, 0, None)
 
 
+def test_same_shape_base_invalidates_sq8_codes(native):
+    """A replacement base of the same shape must drop the codes too: they describe the old rows."""
+    rng = np.random.default_rng(6)
+    base = rng.random((500, 32), dtype=np.float32)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    dev.set_graph(native.Graph.build(base, 0, 32, 100, 4, 100))
+    mn, mx = native.sq8_train(base)
+    dev.set_sq8(native.sq8_encode(base, mn, mx, 4), mn, mx, 2)
+    dev.search_sq8(base[:2], 10, 20, 0, None)
+    other = rng.random((500, 32), dtype=np.float32)
+    dev.set_base(other, 0)
+    with pytest.raises(ValueError, match="no SQ8 codes"):
+        dev.search_sq8(other[:2], 10, 20, 0, None)
+
+
 def test_two_streams_one_index(native, orc):
     """Launches on two HIP streams share the index's scratch (work counter, spill area); the
     engine orders the second call after the first, so both batches come out exact."""

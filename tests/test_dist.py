@@ -120,3 +120,65 @@ def test_packed_keys_order_like_dist_then_id():
     gi, gd = unpack_candidates(torch.sort(pack_candidates(it, dt), 1).values[:, :10])
     mi, md = merge_topk(it, dt + 0.0, 10)
     assert torch.equal(gi, mi) and torch.equal(gd.view(torch.int32), (md + 0.0).view(torch.int32))
+
+
+def _fake_shard(rank, n_per=300, d=8):
+    return np.random.default_rng(100 + rank).random((n_per, d), dtype=np.float32)
+
+
+def _fake_search(rank, k):
+    """A stand-in shard search on CPU tensors: exact top-k of the batch against this rank's rows,
+    (dist, id) order, written into the pipeline's buffers like shard_search_device would."""
+    rows = _fake_shard(rank)
+
+    def fn(q, ids, d, c, stream):
+        qa = q.numpy()
+        dd = ((qa[:, None, :] - rows[None, :, :]) ** 2).sum(-1).astype(np.float32)
+        o = np.stack([np.lexsort((np.arange(rows.shape[0]), r))[:k] for r in dd])
+        ids.copy_(torch.from_numpy(o.astype(np.int32)))
+        d.copy_(torch.from_numpy(np.take_along_axis(dd, o, 1)))
+        c.zero_()
+
+    return fn
+
+
+def _pipeline_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+
+    from alayalite_amd.sharded import ShardPipeline
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(7)
+    batches = [torch.from_numpy(rng.random((23, 8), dtype=np.float32)) for _ in range(5)]
+    pipe = ShardPipeline(_fake_search(rank, 10), 23, 10, rank * 300, "cpu")
+    over = pipe.run(batches)
+    sync = pipe.run_sync(batches)
+    if rank == 0:
+        np.savez(out_path, over_i=np.stack([o[0].numpy() for o in over]), over_d=np.stack([o[1].numpy() for o in over]),
+                 sync_i=np.stack([o[0].numpy() for o in sync]), sync_d=np.stack([o[1].numpy() for o in sync]),
+                 q=np.stack([b.numpy() for b in batches]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_pipeline_gloo(tmp_path):
+    """ShardPipeline (double-buffered batches: search i+1 issued before exchange i) returns, batch
+    for batch, what the synchronous loop and the numpy merge restatement return."""
+    import torch.multiprocessing as mp
+
+    from alayalite_amd.sharded import merge_reference
+
+    out = str(tmp_path / "pipe.npz")
+    mp.spawn(_pipeline_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    assert np.array_equal(got["over_i"], got["sync_i"]) and np.array_equal(got["over_d"], got["sync_d"])
+    for b in range(got["q"].shape[0]):
+        parts = []
+        for r in range(2):
+            ids = torch.empty((23, 10), dtype=torch.int32)
+            d = torch.empty((23, 10), dtype=torch.float32)
+            _fake_search(r, 10)(torch.from_numpy(got["q"][b]), ids, d, torch.empty((23, 4), dtype=torch.int32), 0)
+            parts.append((ids.numpy(), d.numpy()))
+        ref_i, ref_d = merge_reference([p[0] for p in parts], [p[1] for p in parts], [0, 300], 10)
+        assert np.array_equal(got["over_i"][b], ref_i) and np.array_equal(got["over_d"][b], ref_d)

@@ -123,6 +123,39 @@ def test_flat_ties_and_fallback(native, orc):
     assert (ids == np.arange(10, dtype=np.uint32)).all()
 
 
+def test_flat_spin_abort_is_flagged_and_redone(native, orc, flat_mode, monkeypatch):
+    """The warp-specialised scan gives up on an LDS flag after ALAYA_FLAT_SPIN_LIMIT polls: its
+    consumers then write unprovable shortlists.  Forced with a zero limit, the device entry flags
+    every query of an aborted consumer (aligned blocks of 32 queries, all or none), and flat_search's
+    exhaustive redo still returns the exact answer."""
+    import torch
+
+    if flat_mode != "split":
+        pytest.skip("the ring protocol belongs to the split (warp-specialised) scan")
+    monkeypatch.setenv("ALAYA_FLAT_SPIN_LIMIT", "0")
+    rng = np.random.default_rng(44)
+    base = np.ascontiguousarray(rng.random((20000, 128), dtype=np.float32))
+    q = np.ascontiguousarray(rng.random((256, 128), dtype=np.float32))
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    d0 = torch.device("cuda", 0)
+    qd = torch.from_numpy(q).to(d0)
+    ids_d = torch.empty((256, 10), dtype=torch.int32, device=d0)
+    dd = torch.empty((256, 10), dtype=torch.float32, device=d0)
+    flags = torch.zeros((256,), dtype=torch.int32, device=d0)
+    s = torch.cuda.current_stream(d0)
+    dev.flat_search_device(qd.data_ptr(), 256, 10, ids_d.data_ptr(), dd.data_ptr(), flags.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    f = flags.cpu().numpy().reshape(-1, 32)
+    assert f.sum() > 0  # 20k rows of 32-row tiles: a zero poll limit trips on some hand-over
+    assert ((f == 0).all(1) | (f != 0).all(1)).all()
+    ids, dists, redo = dev.flat_search(q[:16], 10)
+    ref_i, ref_d = _exact(orc, base, q[:16], 10)
+    assert redo > 0
+    assert np.array_equal(ids, ref_i)
+    assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+
+
 def test_flat_duplicates_sift_like(native, orc):
     rng = np.random.default_rng(2)
     base = rng.integers(0, 4, (3000, 32)).astype(np.float32)  # many exact ties

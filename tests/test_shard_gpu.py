@@ -27,14 +27,14 @@ def _free_port():
     return port
 
 
-def _run_ranks(tmp_path, world, n, dim, nq, k, ef, seed):
+def _run_ranks(tmp_path, world, n, dim, nq, k, ef, seed, mode="f32"):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "shard_worker.py"), str(tmp_path),
-                                       str(n), str(dim), str(nq), str(k), str(ef), str(seed)], env=env))
+                                       str(n), str(dim), str(nq), str(k), str(ef), str(seed), mode], env=env))
     try:
         rcs = [p.wait(timeout=240) for p in procs]
     finally:
@@ -50,10 +50,11 @@ def _check(parts, k):
 
     ref_i, ref_d = merge_reference([p["shard_ids"] for p in parts], [p["shard_d"] for p in parts],
                                    [int(p["lo"]) for p in parts], k)
-    for p in parts:  # every rank holds the same merged result
-        got_i = p["merged_ids"].astype(np.int64) & 0xFFFFFFFF
-        assert np.array_equal(got_i, ref_i)
-        assert np.array_equal(p["merged_d"].view(np.uint32), ref_d.view(np.uint32))
+    for p in parts:  # every rank holds the same merged result, in one batch and pipelined
+        for ki, kd in (("merged_ids", "merged_d"), ("pipe_ids", "pipe_d")):
+            got_i = p[ki].astype(np.int64) & 0xFFFFFFFF
+            assert np.array_equal(got_i, ref_i), ki
+            assert np.array_equal(p[kd].view(np.uint32), ref_d.view(np.uint32)), kd
     return ref_i
 
 
@@ -73,3 +74,18 @@ def test_sharded_tiny_shards_empty_slots(tmp_path):
     ids = _check(parts, 10)
     assert (ids[:, :10] != EMPTY).all()  # 13 rows >= k = 10: the merged result holds only real rows
     assert set(ids.ravel().tolist()) <= set(range(13))
+
+
+def test_sharded_sq8_ip_two_ranks(tmp_path):
+    """Config 5's path in two shards: d = 768, IP, 24k unit-sphere rows, each shard with its own SQ8
+    space; per shard the SQ8 graph search plus PyIndex::rerank (alaya_index_shard_search_sq8_device),
+    whose ef - k id-0 entries belong to the shard holding global row 0 only.  Merged ids and distance
+    bits equal merge_reference over the restatement's per-shard SQ8 search + rerank."""
+    parts = _run_ranks(tmp_path, 2, 24000, 768, 32, 10, 64, 21, "sq8")
+    ids = _check(parts, 10)
+    lo1 = int(parts[1]["lo"])
+    assert (ids >= lo1).any() and (ids < lo1).any()  # both shards contribute
+    # query 0 sits on global row 0: the reference quirk may repeat row 0 (shard 0's zero entries);
+    # query 1 sits on shard 1's local row 0 = global row lo1, which must appear exactly once
+    assert ids[0, 0] == 0
+    assert (ids[1] == lo1).sum() == 1

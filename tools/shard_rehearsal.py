@@ -1,12 +1,13 @@
 """One-GPU rehearsal of bench.py --mode shard at G = 1, 2, 4, 8 (8-GPU runs are the driver's).
 
-For each G: build (or load) the G base-range shard graphs exactly as bench.py's ranks do, search
+For each G: build the G base-range shard graphs on the device exactly as bench.py's ranks do
+(alaya_index_build_graph, deterministic), search
 every shard on this GPU in turn, merge the per-shard top-k by (dist, global id) with the same
 merge the ranks use, pick the smallest ef of the sweep whose merged recall@10 >= 0.95, and time
 each shard's kernel at that ef.  Predicted G-GPU QPS = nq / max over shards of the kernel time
 (the all-gather of nq*k*8 B per rank and the merge are measured separately by bench.py).
 
-usage: python tools/shard_rehearsal.py [--n 1000000] [--nq 1000] [--gs 1,2,4,8]
+usage: python tools/shard_rehearsal.py [--n 1000000] [--nq 10000] [--gs 1,2,4,8]   (config 4: 10k queries)
 """
 
 import argparse
@@ -24,7 +25,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
-    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--nq", type=int, default=10000)
     ap.add_argument("--dim", type=int, default=960)
     ap.add_argument("--gs", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
@@ -40,10 +41,8 @@ def main():
     ext = _native._ext
     dev = torch.device("cuda", 0)
     base, queries = gist_like(args.n, args.nq, args.dim)
-    base_dev = torch.from_numpy(base).to(dev)
     q_dev = torch.from_numpy(queries).to(dev)
-    gt = b.exact_gt(torch, base_dev, q_dev, base, queries)
-    del base_dev
+    gt, _ = b.exact_gt_flat(ext, base, queries, 0)
     torch.cuda.empty_cache()
     nq, K = args.nq, b.K
     results = []
@@ -51,15 +50,13 @@ def main():
         shards = []
         for r in range(G):
             lo, hi = shard_range(args.n, G, r)
-            tag = "gist" if G == 1 else f"gist_shard{r}of{G}"
             sb = np.ascontiguousarray(base[lo:hi])
-            g, build_s = b.graph_for(ext, sb, 100, b.host_threads(), os.path.join(ROOT, "data_cache"), tag)
             ix = ext.DeviceIndex(0)
             ix.set_base(sb, 0)
-            ix.set_graph(g)
+            t = time.time()
+            ix.build_graph(b.R, 100, 100, 0, 0, 2)
             shards.append((lo, ix))
-            print(f"G={G} shard {r}: rows [{lo},{hi}) graph {'built' if build_s else 'cached'} {build_s:.1f}s",
-                  flush=True)
+            print(f"G={G} shard {r}: rows [{lo},{hi}) device graph {time.time() - t:.1f}s", flush=True)
         ids = torch.empty((nq, K), dtype=torch.int32, device=dev)
         dd = torch.empty((nq, K), dtype=torch.float32, device=dev)
         cnt = torch.empty((nq, 4), dtype=torch.int32, device=dev)
@@ -70,8 +67,8 @@ def main():
             for lo, ix in shards:
                 a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(stream)
-                ix.search_device(q_dev.data_ptr(), nq, K, ef, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(),
-                                 stream.cuda_stream)
+                ix.shard_search_device(q_dev.data_ptr(), nq, K, ef, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(),
+                                       stream.cuda_stream)
                 e.record(stream)
                 torch.cuda.synchronize()
                 times.append(a.elapsed_time(e))
