@@ -128,6 +128,7 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
   const uint32_t hsize = 1u << p.hash_log2;
   const uint64_t bit_words = (p.n + 31) / 32;
   uint32_t *slot_bits = p.overflow_bits + static_cast<uint64_t>(blockIdx.x) * bit_words;
+  uint32_t *slot_dirty = p.dirty_words + static_cast<uint64_t>(blockIdx.x) * p.dirty_cap;
   const uint32_t W = level_width(p, bp.level);
 
   for (;;) {
@@ -147,7 +148,7 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
       L.pi[e] = 0u;
     }
     wave_sync();
-    Visited vs = make_visited(p, L.hash, slot_bits);
+    Visited vs = make_visited(p, L.hash, slot_bits, slot_dirty);
     PoolState ps{0u, 0u, p.ef};
 
     // entry: the point's first searched level starts from the greedy descent, lower levels from
@@ -191,9 +192,9 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
       L.pi[0] = u;
     }
     ps.size = 1;
-    visit(vs, u, lane == 0, bit_words);
+    visit(vs, u, lane == 0);
     // the point itself is reachable in a refine pass: never a candidate of its own
-    if (u != pt) visit(vs, pt, lane == 0, bit_words);
+    if (u != pt) visit(vs, pt, lane == 0);
     wave_sync();
 
     while (ps.cur < ps.size) {
@@ -202,8 +203,8 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
       const uint32_t v = lane < static_cast<int>(W) ? row[lane] : kEmpty;
       const int cnt = static_cast<int>(row_count(v, W));
       const bool act = lane < cnt;
-      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
-      const bool fresh = visit(vs, v, act, bit_words);
+      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs);
+      const bool fresh = visit(vs, v, act);
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
       if (nf == 0) continue;
@@ -222,6 +223,7 @@ __global__ void __launch_bounds__(64) build_search_kernel(BuildParams bp) {
       bp.cand_d[static_cast<uint64_t>(qi) * p.ef + i] = L.pd[i];
     }
     if (lane == 0) bp.cand_n[qi] = ps.size;
+    visit_end(vs);
     wave_sync();
   }
 }
@@ -420,7 +422,7 @@ hipError_t launch(Which w, const BuildParams &p, int grid, size_t lds, hipStream
 }  // namespace
 
 size_t build_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact) {
-  return search_lds_bytes(stride, ef, hash_log2, false, compact);
+  return search_wave_lds_bytes(stride, ef, hash_log2, compact);
 }
 
 hipError_t build_search_occupancy(const BuildParams &p, size_t lds, int *blocks_per_cu) {

@@ -119,7 +119,8 @@ struct alaya_index {
   bool norms_ready = false;
   float max_norm = 0.f;
   // scratch
-  DevBuf work, overflow, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
+  DevBuf work, overflow, dirty, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
+  size_t overflow_clean = 0;  // leading bytes of `overflow` known to be zero (kernels leave it clean)
   uint32_t hash_log2_override = 0;
   int visited_mode_override = 0;  // 0 auto, 1 compact 16-bit slots, 2 wide 32-bit slots,
                                   // 3 compact with probes capped at 2 (exercises the probe spill)
@@ -176,16 +177,50 @@ SearchParams base_params(alaya_index *ix) {
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr uint32_t kDirtyCap = 16384;  // per-slot dirty-word list (64 KB): words a spilled query set
 
-// Size the LDS visited table for residency: the batch wants ceil(nq / CUs) resident queries per
-// CU (capped by what the register file admits); the table takes what LDS is left per query,
-// never more than ~2x the expected visited count (~24 ids per expansion x ef), never below
+// The visited set's second level for `slots` persistent searchers over ix->n rows: one clean N-bit
+// bitset per slot (zeroed once when allocated; every query leaves it clean) and a dirty-word list.
+void prepare_spill(alaya_index *ix, SearchParams &p, uint64_t slots, hipStream_t stream) {
+  const uint64_t words = (ix->n + 31) / 32;
+  const size_t bytes = static_cast<size_t>(std::max<uint64_t>(slots, 1)) * words * 4;
+  if (bytes > ix->overflow.bytes) {
+    ix->overflow.reserve(bytes);
+    ix->overflow_clean = 0;
+  }
+  if (ix->overflow_clean < ix->overflow.bytes) {
+    hip_check(hipMemsetAsync(ix->overflow.ptr, 0, ix->overflow.bytes, stream), "hipMemsetAsync");
+    ix->overflow_clean = ix->overflow.bytes;
+  }
+  uint32_t cap = kDirtyCap;
+  if (const char *e = std::getenv("ALAYA_DIRTY_CAP")) cap = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));  // tests
+  ix->dirty.reserve(static_cast<size_t>(std::max<uint64_t>(slots, 1)) * std::max<uint32_t>(cap, 1) * 4);
+  p.overflow_bits = ix->overflow.as<uint32_t>();
+  p.dirty_words = ix->dirty.as<uint32_t>();
+  p.dirty_cap = cap;
+}
+
+// Waves per search workgroup: SQ8 searchers share the quantizer's per-dimension scale and min
+// (search_shared_lds_bytes) across 4 waves, one per SIMD; f32 searchers have nothing to share.
+// ALAYA_SEARCH_WAVES overrides (1, 2 or 4; diagnostics).
+int search_waves(const SearchParams &p) {
+  if (const char *e = std::getenv("ALAYA_SEARCH_WAVES")) {
+    const int w = std::atoi(e);
+    if (w == 1 || w == 2 || w == 4) return w;
+  }
+  return p.sq8_order != 0 ? 4 : 1;
+}
+
+// Size the LDS visited table for residency: the batch wants ceil(nq / CUs) resident queries
+// (waves) per CU (capped by what the register file admits); the table takes what LDS is left per
+// wave, never more than ~2x the expected visited count (~24 ids per expansion x ef), never below
 // 1024 slots.  A query that outgrows its table spills to the global bitset (exact either way).
 // Layout: compact 16-bit slots (twice the entries per byte) whenever the ids' hash remainder fits
-// (log2 n - log2 slots <= 11), else 32-bit id slots.  Returns log2 slots; sets p.vis_*.
+// (log2 n - log2 slots <= 11), else 32-bit id slots.  A workgroup of W waves also holds the shared
+// region, counted per wave as shared / W.  Returns log2 slots; sets p.vis_*.
 constexpr uint32_t kMaxCompactRbits = 11;
 
-uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef) {
+uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef, int W = 1) {
   const uint32_t lbits = std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2)));
   const int mode = ix->visited_mode_override;  // 0 auto, 1 compact, 2 wide, 3 compact + short probes
   auto set_mode = [&](uint32_t l, bool compact) {
@@ -202,30 +237,36 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     if (compact && !fits_compact(l)) throw ArgError("compact visited table cannot encode ids of this index");
     return set_mode(l, compact);
   }
-  const size_t fixed = alaya_amd::search_lds_bytes(ix->stride, ef, 0, p.sq8_order != 0) - 4;
+  const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0);
+  const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
+  const size_t fixed = wave_fixed + (shared + W - 1) / W;  // per wave
   int vgpr_blocks = 0;
-  hip_check(alaya_amd::search_occupancy(p, fixed + 4096, &vgpr_blocks), "occupancy");
-  vgpr_blocks = std::max(1, vgpr_blocks);
+  hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + 4096), &vgpr_blocks), "occupancy");
+  const uint64_t vgpr_waves = static_cast<uint64_t>(std::max(1, vgpr_blocks)) * W;
   const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
-  uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_blocks, want));
+  uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_waves, want));
   const uint32_t cap = ceil_log2(48ull * ef);
-  if (want > static_cast<uint64_t>(vgpr_blocks)) {
+  if (want > vgpr_waves) {
     // Several queries per resident slot: residency beyond what keeps a table of ~32 ef slots
     // (load <= ~0.5 at the usual 10-24 ef visited ids) costs more in probes and spills than it
     // gains (SIFT 1M, 10k queries: 4 waves/SIMD with 8 KB tables beat 5 with 4 KB by ~20 %).
     uint32_t tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(32ull * ef)));
-    auto per_block = [&](uint32_t l) {
+    if (const char *e = std::getenv("ALAYA_VISITED_TABLE_EF")) {  // diagnostics: slots per ef target
+      const uint64_t f = std::strtoull(e, nullptr, 10);
+      if (f) tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(f * ef)));
+    }
+    auto per_wave = [&](uint32_t l) {
       const bool tc = mode != 2 && fits_compact(l);
       return fixed + (static_cast<size_t>(tc ? 2 : 4) << l);
     };
     // ... but never leave a SIMD without a wave for it: halve the table (down to ~16 ef slots)
-    // while fewer than one block per SIMD would fit (10M x 768 SQ8 at ef 340: 32 KB tables admit
+    // while fewer than one wave per SIMD would fit (10M x 768 SQ8 at ef 340: 32 KB tables admit
     // 3 of the 4 waves the register file allows)
-    const uint64_t simd_floor = std::min<uint64_t>(4, static_cast<uint64_t>(vgpr_blocks));
-    while (kLdsPerCu / per_block(tl) < simd_floor && tl > 10 && (1ull << (tl - 1)) >= 16ull * ef) --tl;
-    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kLdsPerCu / per_block(tl)));
+    const uint64_t simd_floor = std::min<uint64_t>(4, vgpr_waves);
+    while (kLdsPerCu / per_wave(tl) < simd_floor && tl > 10 && (1ull << (tl - 1)) >= 16ull * ef) --tl;
+    waves = std::max<uint64_t>(1, std::min<uint64_t>(waves, kLdsPerCu / per_wave(tl)));
   }
-  const size_t budget = kLdsPerCu / blocks > fixed ? kLdsPerCu / blocks - fixed : 0;
+  const size_t budget = kLdsPerCu / waves > fixed ? kLdsPerCu / waves - fixed : 0;
   auto pick = [&](size_t slot_bytes, uint32_t lmax) {
     uint32_t l = 10;
     while (l < lmax && (slot_bytes << (l + 1)) <= budget) ++l;
@@ -283,22 +324,26 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.sq_min = ix->sq_min.as<float>();
     p.sq_max = ix->sq_max.as<float>();
   }
-  p.hash_log2 = size_visited(ix, p, nq, ef);
-  const size_t lds = alaya_amd::search_lds_bytes(ix->stride, ef, p.hash_log2, sq8, p.vis_rbits != alaya_amd::kVisWide);
-  if (lds > 160 * 1024) throw ArgError("ef / dim too large for the LDS budget");
+  // waves per workgroup: never more than the batch needs
+  int W = search_waves(p);
+  while (W > 1 && static_cast<uint64_t>(W) > nq) W /= 2;
+  p.hash_log2 = size_visited(ix, p, nq, ef, W);
+  const bool compact = p.vis_rbits != alaya_amd::kVisWide;
+  p.wave_lds = static_cast<uint32_t>(alaya_amd::search_wave_lds_bytes(ix->stride, ef, p.hash_log2, compact));
+  const size_t lds = alaya_amd::search_shared_lds_bytes(ix->stride, sq8) + static_cast<size_t>(W) * p.wave_lds;
+  if (lds > kLdsPerCu) throw ArgError("ef / dim too large for the LDS budget");
   int per_cu = 0;
-  hip_check(alaya_amd::search_occupancy(p, lds, &per_cu), "occupancy");
+  hip_check(alaya_amd::search_occupancy(p, W, lds, &per_cu), "occupancy");
   per_cu = std::max(1, per_cu);
-  const uint64_t grid64 = std::min<uint64_t>(nq, static_cast<uint64_t>(per_cu) * ix->num_cus);
+  const uint64_t blocks_needed = (nq + W - 1) / W;
+  const uint64_t grid64 = std::min<uint64_t>(blocks_needed, static_cast<uint64_t>(per_cu) * ix->num_cus);
   const int grid = static_cast<int>(std::max<uint64_t>(1, grid64));
-  const uint64_t words = (ix->n + 31) / 32;
-  ix->overflow.reserve(static_cast<size_t>(grid) * words * 4);
-  ix->work.reserve(4);
-  p.overflow_bits = ix->overflow.as<uint32_t>();
-  p.work_counter = ix->work.as<uint32_t>();
   scratch_acquire(ix, stream);
+  prepare_spill(ix, p, static_cast<uint64_t>(grid) * W, stream);
+  ix->work.reserve(4);
+  p.work_counter = ix->work.as<uint32_t>();
   hip_check(hipMemsetAsync(p.work_counter, 0, 4, stream), "hipMemsetAsync");
-  hip_check(alaya_amd::launch_search(p, grid, lds, stream), "search launch");
+  hip_check(alaya_amd::launch_search(p, grid, W, lds, stream), "search launch");
   scratch_release(ix, stream);
 }
 
@@ -421,6 +466,52 @@ int alaya_device_count(int *count) {
 }
 
 // ---- graphs ---------------------------------------------------------------------------------
+int alaya_hbm_stream_read(int device, uint64_t bytes, int iters, double *gbs) {
+  return guarded([&] {
+    if (!gbs || bytes < (1u << 20) || iters < 1) throw ArgError("invalid arguments");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) throw DeviceError("no HIP device available");
+    if (device < 0 || device >= count) throw ArgError("device ordinal out of range");
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    hipDeviceProp_t prop;
+    hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+    bytes = bytes / 16 * 16;
+    DevBuf buf, sink;
+    buf.reserve(bytes);
+    sink.reserve(4);
+    hipStream_t s = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
+    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipEventCreate(&a), "hipEventCreate");
+    hip_check(hipEventCreate(&b), "hipEventCreate");
+    double best = 0.0;
+    try {
+      hip_check(hipMemsetAsync(buf.ptr, 0, bytes, s), "memset");
+      const int grid = prop.multiProcessorCount * 8;
+      hip_check(alaya_amd::launch_stream_read(buf.ptr, bytes, grid, sink.as<float>(), s), "stream read");  // warm
+      for (int it = 0; it < iters; ++it) {
+        hip_check(hipEventRecord(a, s), "hipEventRecord");
+        hip_check(alaya_amd::launch_stream_read(buf.ptr, bytes, grid, sink.as<float>(), s), "stream read");
+        hip_check(hipEventRecord(b, s), "hipEventRecord");
+        hip_check(hipEventSynchronize(b), "hipEventSynchronize");
+        float ms = 0.f;
+        hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+        best = std::max(best, static_cast<double>(bytes) / (ms * 1e6));
+      }
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+      (void)hipStreamDestroy(s);
+      throw;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipStreamDestroy(s);
+    *gbs = best;
+  });
+}
+
 int alaya_graph_build_hnsw(const float *data, uint64_t n, uint32_t dim, int metric, uint32_t R,
                            uint32_t ef_construction, uint32_t num_threads, uint64_t seed,
                            alaya_graph **out) {
@@ -589,6 +680,7 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     ix->metric = metric;
     ix->generic = generic;
     ix->overflow.release();
+    ix->overflow_clean = 0;
     ix->norms_ready = false;
     ix->capacity = n;
     ix->upd_graph.reset();
@@ -1057,9 +1149,7 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
     hip_check(alaya_amd::build_search_occupancy(bp, lds, &per_cu), "occupancy");
     per_cu = std::max(1, per_cu);
     const uint64_t grid_max = static_cast<uint64_t>(per_cu) * ix->num_cus;
-    const uint64_t words = (n + 31) / 32;
-    ix->overflow.reserve(static_cast<size_t>(std::min<uint64_t>(grid_max, bmax)) * words * 4);
-    bp.s.overflow_bits = ix->overflow.as<uint32_t>();
+    prepare_spill(ix, bp.s, std::min<uint64_t>(grid_max, bmax), st);
 
     hip_check(hipEventRecord(e0, st), "event");
     uint64_t launches = 0;

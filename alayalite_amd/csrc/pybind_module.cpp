@@ -995,4 +995,9 @@ PYBIND11_MODULE(_alayalitepy, m) {
     check(alaya_device_count(&c));
     return c;
   });
+  m.def("hbm_stream_read", [](int device, uint64_t bytes, int iters) {
+    double gbs = 0.0;
+    check(alaya_hbm_stream_read(device, bytes, iters, &gbs));
+    return gbs;
+  }, py::arg("device") = 0, py::arg("bytes") = 4ull << 30, py::arg("iters") = 5);
 }

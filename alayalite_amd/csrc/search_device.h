@@ -325,11 +325,14 @@ __device__ __forceinline__ void sq8_chunk(const float *xq, const float *sc, cons
   acc[3] = sq8_term<kIP>(x.w, s.w, mn.w, static_cast<float>(w >> 24), acc[3]);
 }
 
+#ifndef ALAYA_SQ8_DW
+#define ALAYA_SQ8_DW 48  // code dwords in flight per lane (rows per lane group = DW / chunks)
+#endif
 // rows per lane group per pass: <= 48 code dwords in flight per lane (the per-chunk float4 LDS
 // reads are hoisted too; more rows spill at d = 768)
 template <int kOrder, int kFull>
 constexpr int sq8_rows_per_group() {
-  return kFull <= 0 ? 1 : (48 / kFull >= 4 ? 4 : (48 / kFull < 1 ? 1 : 48 / kFull));
+  return kFull <= 0 ? 1 : (ALAYA_SQ8_DW / kFull >= 4 ? 4 : (ALAYA_SQ8_DW / kFull < 1 ? 1 : ALAYA_SQ8_DW / kFull));
 }
 
 // One pass of SQ8 code loads in registers (compile-time chunk count): lane group g takes rows
@@ -386,12 +389,30 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
   const bool half = rem >= P / 2;
   const int tail_begin = P * kFull + (half ? P / 2 : 0);
   float acc[SP::kR][4];
+  int live = 0;  // wave-uniform number of row slots in use
 #pragma unroll
   for (int r = 0; r < SP::kR; ++r) {
     acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0.f;
-    if (base + G * r >= n) break;  // wave-uniform
+    live += base + G * r < n ? 1 : 0;
+  }
+  // chunk-major: a chunk's query / scale / min values feed every row slot, then die
 #pragma unroll
-    for (int t = 0; t < kFull; ++t) sq8_chunk<kIP>(xq, sc, mnv, P * t + 4 * m, S.w[r][t], acc[r]);
+  for (int t = 0; t < kFull; ++t) {
+    const int e = P * t + 4 * m;
+    const float4 x = *reinterpret_cast<const float4 *>(xq + e);
+    const float4 s = *reinterpret_cast<const float4 *>(sc + e);
+    float4 mn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (kIP) mn = *reinterpret_cast<const float4 *>(mnv + e);
+#pragma unroll
+    for (int r = 0; r < SP::kR; ++r) {
+      if (r >= live) break;
+      const uint32_t w = S.w[r][t];
+      float *a = acc[r];
+      a[0] = sq8_term<kIP>(x.x, s.x, mn.x, static_cast<float>(w & 0xffu), a[0]);
+      a[1] = sq8_term<kIP>(x.y, s.y, mn.y, static_cast<float>((w >> 8) & 0xffu), a[1]);
+      a[2] = sq8_term<kIP>(x.z, s.z, mn.z, static_cast<float>((w >> 16) & 0xffu), a[2]);
+      a[3] = sq8_term<kIP>(x.w, s.w, mn.w, static_cast<float>(w >> 24), a[3]);
+    }
   }
 #pragma unroll
   for (int r = 0; r < SP::kR; ++r) {
@@ -518,7 +539,14 @@ __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds
 //              stores 1 + (probe distance << rbits | low rbits bits of h), so (slot, entry)
 //              identifies v exactly in half the bytes: twice the entries per LDS byte.
 // When the table passes its load limit (or a compact probe would exceed the encodable distance)
-// the query spills: a per-slot global N-bit bitset becomes the second level (atomicOr).
+// the query spills: a per-slot global N-bit bitset becomes the second level (atomicOr), and the
+// LDS table stays as a read-only first level.
+// The bitset is clean (all zero) whenever no query owns the slot, and is cleared lazily: the
+// atomicOr that sets the first bit of a word returns 0, and that lane appends the word's index to
+// the slot's dirty list (one append per touched word, ballot + prefix count).  At the query's end
+// the wave zeroes exactly the listed words -- O(words touched), not the N/8 bytes of the whole
+// bitset (1.25 MB at 10M rows) that a spilling query used to clear first.  A list that outgrows
+// its capacity falls back to clearing the whole bitset.  No extra round trip per visit.
 // --------------------------------------------------------------------------------------------
 struct Visited {
   uint32_t *tab;
@@ -526,20 +554,29 @@ struct Visited {
   uint32_t count;        // wave-uniform number of entries in the LDS table
   uint32_t limit;        // switch to the global bitset above this many entries
   bool spilled;          // wave-uniform
-  uint32_t *bits;        // per-slot global bitset (valid when spilled)
+  uint32_t *bits;        // per-slot global bitset (clean on entry, cleaned by visit_end)
+  uint32_t *dirty;       // per-slot list of the bitset words this query set (dirty_cap entries)
+  uint32_t dirty_cap;
+  uint32_t ndirty;       // wave-uniform number of words appended (may exceed dirty_cap)
+  uint64_t n_words;      // bitset words (ceil(n / 32))
   uint32_t rbits;        // compact: remainder bits; kVisWide: 32-bit slots
   uint32_t lmask;        // compact: 2^L - 1
   uint32_t lshift;       // compact, L < log2h: home = h << lshift
   uint32_t max_disp;     // compact: largest encodable probe distance
 };
 
-__device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t *tab, uint32_t *bits) {
+__device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t *tab, uint32_t *bits,
+                                                uint32_t *dirty) {
   Visited vs;
   vs.tab = tab;
   vs.log2h = p.hash_log2;
   vs.count = 0u;
   vs.spilled = false;
   vs.bits = bits;
+  vs.dirty = dirty;
+  vs.dirty_cap = p.dirty_cap;
+  vs.ndirty = 0u;
+  vs.n_words = (p.n + 31) / 32;
   vs.rbits = p.vis_rbits;
   const uint32_t hsize = 1u << p.hash_log2;
   if (p.vis_rbits == kVisWide) {
@@ -620,37 +657,58 @@ __device__ __forceinline__ int table_insert(const Visited &vs, uint32_t v) {
   return 2;
 }
 
-__device__ void spill_begin(Visited &vs, uint64_t n_words) {
-  // zero this slot's global bitset once, then keep the LDS table as a read-only first level.
-  const int lane = lane_id();
-  for (uint64_t w = lane; w < n_words; w += 64) vs.bits[w] = 0u;
-  __threadfence_block();
-  wave_sync();
-  vs.spilled = true;
-}
-
-__device__ __forceinline__ bool global_visit(const Visited &vs, uint32_t v) {
-  const uint32_t bit = 1u << (v & 31);
-  const uint32_t old = atomicOr(&vs.bits[v >> 5], bit);
-  return (old & bit) == 0u;
-}
+// The global bitset becomes the second level; it is already clean (no zeroing here).
+__device__ __forceinline__ void spill_begin(Visited &vs) { vs.spilled = true; }
 
 // All lanes with `act` insert their v; duplicates among lanes must have been removed.
-__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, uint64_t n_words) {
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
   bool fresh = false;
+  bool global = false;
   if (!vs.spilled) {
     int r = 0;
     if (act) r = table_insert(vs, v);
     fresh = r == 1;
     vs.count += __popcll(ballot(fresh));
     if (ballot(r == 2)) {  // a compact probe ran out of encodable distance: spill now
-      spill_begin(vs, n_words);
-      if (r == 2) fresh = global_visit(vs, v);
+      spill_begin(vs);
+      global = r == 2;
     }
   } else if (act) {
-    if (!table_lookup(vs, v)) fresh = global_visit(vs, v);
+    global = !table_lookup(vs, v);
+  }
+  if (vs.spilled) {  // wave-uniform
+    const uint32_t bit = 1u << (v & 31);
+    uint32_t old = bit;
+    if (global) {
+      old = atomicOr(&vs.bits[v >> 5], bit);
+      fresh = (old & bit) == 0u;
+    }
+    // the lane that set a word's first bit records the word (at most one lane per word: the
+    // atomics of one wave to one word are serialised, the later ones see the earlier bits)
+    const bool first = global && old == 0u;
+    const uint64_t fm = ballot(first);
+    if (fm) {
+      const uint32_t pos = vs.ndirty + __popcll(fm & ((1ull << lane_id()) - 1ull));
+      if (first && pos < vs.dirty_cap) vs.dirty[pos] = v >> 5;
+      vs.ndirty += __popcll(fm);
+    }
   }
   return fresh;
+}
+
+// End of a query: leave the slot's bitset clean for the next one (the words on the dirty list, or
+// the whole bitset when the list overflowed).  Wave-uniform.
+__device__ __forceinline__ void visit_end(Visited &vs) {
+  if (!vs.spilled) return;
+  const int lane = lane_id();
+  __threadfence_block();  // this wave's dirty-list stores are visible to its own loads below
+  if (vs.ndirty <= vs.dirty_cap) {
+    for (uint32_t i = lane; i < vs.ndirty; i += 64) vs.bits[vs.dirty[i]] = 0u;
+  } else {
+    for (uint64_t w = lane; w < vs.n_words; w += 64) vs.bits[w] = 0u;
+  }
+  __threadfence_block();  // the clearing stores land before the slot's next query sets bits
+  vs.spilled = false;
 }
 
 // --------------------------------------------------------------------------------------------

@@ -43,7 +43,10 @@ struct SearchParams {
                           // distance 0.0; 0xffffffff = empty slot, with distance FLT_MAX)
   // scratch
   uint32_t *work_counter; // zeroed before each launch
-  uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area
+  uint32_t *overflow_bits;// grid x ceil(n/32) words: visited-set spill area, all zero between queries
+  uint32_t *dirty_words;  // slots x dirty_cap: per-slot list of the spill-area words a query set
+  uint32_t dirty_cap;
+  uint32_t wave_lds;      // bytes of one wave's LDS region (search_wave_lds_bytes)
   uint32_t hash_log2;     // LDS visited table = 1 << hash_log2 slots
   // visited-table layout: kVisWide = 32-bit id slots; otherwise 16-bit compact slots holding
   // (probe distance, low vis_rbits bits of a vis_lbits-bit bijective hash) -- exact either way
@@ -79,17 +82,25 @@ struct RerankParams {
 };
 
 constexpr uint32_t kVisWide = 0xffffffffu;
-// bytes of the LDS visited table / of the whole per-workgroup LDS footprint
+// bytes of the LDS visited table / of one wave's LDS region / of a workgroup's shared region
+// (SQ8: the quantizer's per-dimension scale and min); a workgroup of W waves takes
+// shared + W * wave bytes
 inline size_t visited_table_bytes(uint32_t hash_log2, bool compact) {
   return (static_cast<size_t>(compact ? 2 : 4)) << hash_log2;
 }
-size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8 = false, bool compact = false);
+size_t search_wave_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact = false);
+__host__ __device__ inline size_t search_shared_lds_bytes(uint32_t stride, bool sq8) {
+  return sq8 ? 2 * static_cast<size_t>(stride) * 4 : 0;
+}
 // rerank: p.base/p.queries are the raw f32 rows and the (normalised) f32 queries
 hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream);
-hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu);
-hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream);
+hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu);
+hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream);
 // out[q * n + i] = dist(queries[q], base[ids[i]]) for q < nq (bit-exact device distance)
 hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint32_t n,
                                 uint32_t nq, float *out, hipStream_t stream);
+
+// streaming read of `bytes` (multiple of 16) for the measured-bandwidth calibration
+hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, float *sink, hipStream_t stream);
 
 }  // namespace alaya_amd

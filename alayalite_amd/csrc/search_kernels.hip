@@ -26,11 +26,13 @@ namespace alaya_amd {
 
 namespace {
 
-// LDS layout of a search workgroup (search_lds_bytes below is its size).
+// LDS layout of a search workgroup of W waves: a shared region (SQ8: the per-index scale and min
+// of SQ8Space's quantizer, identical for every query, stored once per workgroup) followed by one
+// region of p.wave_lds bytes per wave (query, candidate batch, pool, visited table).
 template <int kSpace>
-__device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *smem) {
+__device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *smem, int wave) {
   Lds L;
-  unsigned char *ptr = smem;
+  unsigned char *ptr = smem + search_shared_lds_bytes(p.stride, kSpace != 0) + static_cast<size_t>(wave) * p.wave_lds;
   L.q = reinterpret_cast<float *>(ptr);
   ptr += static_cast<size_t>(p.stride) * 4;
   L.cid = reinterpret_cast<uint32_t *>(ptr);
@@ -44,18 +46,35 @@ __device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *s
   L.pi = reinterpret_cast<uint32_t *>(ptr);
   ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
   L.hash = reinterpret_cast<uint32_t *>(ptr);
-  ptr += static_cast<size_t>(p.vis_rbits != kVisWide ? 2 : 4) << p.hash_log2;
-  L.sq_scale = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
-  ptr += kSpace ? static_cast<size_t>(p.stride) * 4 : 0;
-  L.sq_min = kSpace ? reinterpret_cast<float *>(ptr) : nullptr;
+  L.sq_scale = kSpace ? reinterpret_cast<float *>(smem) : nullptr;
+  L.sq_min = kSpace ? reinterpret_cast<float *>(smem) + p.stride : nullptr;
   return L;
+}
+
+// SQ8: the workgroup's waves fill the shared scale / min once (SQ8Quantizer, sq8.hpp:99-130:
+// scale = (max - min) * (1/255)), before any wave starts a query.
+template <int kSpace>
+__device__ __forceinline__ void fill_shared(const SearchParams &p, const Lds &L) {
+  if constexpr (kSpace != 0) {
+    const float kInv255 = 1.0f / 255.0f;
+    for (uint32_t e = threadIdx.x; e < p.stride; e += blockDim.x) {
+      float sc = 0.f, mn = 0.f;
+      if (e < p.dim) {
+        mn = p.sq_min[e];
+        sc = (p.sq_max[e] - mn) * kInv255;
+      }
+      L.sq_scale[e] = sc;
+      L.sq_min[e] = mn;
+    }
+    __syncthreads();
+  }
 }
 
 // Per-query setup shared by the search kernels: the query staged in LDS (SQ8: encoded with the
 // quantizer), visited table and pool cleared, then Graph::initialize_search (graph.hpp:148-158).
 template <bool kIP, int kChunks, int kSpace>
 __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L, uint32_t qi, uint32_t *slot_bits,
-                                            uint64_t bit_words, Visited &vs, PoolState &ps,
+                                            uint32_t *slot_dirty, Visited &vs, PoolState &ps,
                                             uint32_t &n_dist_up, uint32_t &n_hops_up) {
   const int lane = lane_id();
   const uint32_t hsize = 1u << p.hash_log2;
@@ -66,25 +85,22 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
   } else {
     // SQ8Space::QueryComputer encodes the query with the quantizer (sq8_space.hpp:266-271,
     // SQ8Quantizer::quantize sq8.hpp:118-130), then every distance uses its codes.
-    const float kInv255 = 1.0f / 255.0f;
+    // (the per-index scale and min are the workgroup's shared LDS copy, fill_shared)
     for (uint32_t e = lane; e < p.stride; e += 64) {
-      float xq = 0.f, sc = 0.f, mn = 0.f;
+      float xq = 0.f;
       if (e < p.dim) {
         const float v = qsrc[e];
-        mn = p.sq_min[e];
+        const float mn = p.sq_min[e];
         const float mx = p.sq_max[e];
         uint32_t code;
         if (mx == mn) code = 0;
         else if (v >= mx) code = 255;
         else if (v <= mn) code = 0;
         else code = static_cast<uint8_t>(((v - mn) / (mx - mn)) * 255);
-        sc = (mx - mn) * kInv255;
         const float xf = static_cast<float>(code);
-        xq = kIP ? fmaf(xf, sc, mn) : xf;
+        xq = kIP ? fmaf(xf, L.sq_scale[e], mn) : xf;
       }
       L.q[e] = xq;
-      L.sq_scale[e] = sc;
-      L.sq_min[e] = mn;
     }
   }
   {
@@ -97,7 +113,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
     L.pi[e] = 0u;
   }
   wave_sync();
-  vs = make_visited(p, L.hash, slot_bits);
+  vs = make_visited(p, L.hash, slot_bits, slot_dirty);
   ps = PoolState{0u, 0u, p.ef};
 
   // ---- Graph::initialize_search (graph.hpp:148-158) ---------------------------------------
@@ -147,7 +163,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
     }
     ps.size = 1;
     ps.cur = 0;
-    visit(vs, u, lane == 0, bit_words);
+    visit(vs, u, lane == 0);
     wave_sync();
   } else {
     // NSG-style entry points: insert each ep, then mark it visited (graph.hpp:153-156)
@@ -167,8 +183,8 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
       // duplicates among eps are all inserted (no visited check in the reference loop)
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t vj = read_lane(v, j);
-        if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
-        visit(vs, vj, lane == 0, bit_words);
+        if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs);
+        visit(vs, vj, lane == 0);
       }
       wave_sync();
     }
@@ -206,13 +222,20 @@ __device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, c
 // kStamp: diagnostic build that accumulates s_memtime cycles per phase into p.stamps (nq x 8):
 // [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
 // [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] prefetch hits.
+// A workgroup holds blockDim.x / 64 waves (1 for f32 rows, up to 4 for SQ8, which share the
+// quantizer's scale / min); each wave is an independent persistent searcher with its own visited
+// spill slot.  After fill_shared the waves never synchronise again.
 template <bool kIP, int kChunks, bool kStamp, int kSpace = 0>
-__global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
+__global__ void __launch_bounds__(256) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
-  const Lds L = carve_lds<kSpace>(p, smem);
+  const int wave = static_cast<int>(threadIdx.x >> 6);
+  const Lds L = carve_lds<kSpace>(p, smem, wave);
+  fill_shared<kSpace>(p, L);
   const uint64_t bit_words = (p.n + 31) / 32;
-  uint32_t *slot_bits = p.overflow_bits + static_cast<uint64_t>(blockIdx.x) * bit_words;
+  const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
+  uint32_t *slot_bits = p.overflow_bits + slot * bit_words;
+  uint32_t *slot_dirty = p.dirty_words + slot * p.dirty_cap;
 
   for (;;) {
     uint32_t qi = 0;
@@ -233,7 +256,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     Visited vs;
     PoolState ps;
     uint32_t n_dist = 0, n_expand = 0, n_dist_up = 0, n_hops_up = 0;
-    query_begin<kIP, kChunks, kSpace>(p, L, qi, slot_bits, bit_words, vs, ps, n_dist_up, n_hops_up);
+    query_begin<kIP, kChunks, kSpace>(p, L, qi, slot_bits, slot_dirty, vs, ps, n_dist_up, n_hops_up);
 
     // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
     stamp(0);
@@ -269,8 +292,8 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
           if (j < lane && vj == v) act = false;
         }
       }
-      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs, bit_words);
-      const bool fresh = visit(vs, v, act, bit_words);
+      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs);
+      const bool fresh = visit(vs, v, act);
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
       // issue the prefetch only after v is consumed: a use of v behind a younger load would
@@ -310,6 +333,7 @@ __global__ void __launch_bounds__(64) hnsw_search_kernel(SearchParams p) {
     }
 
     query_end(p, L, ps, qi, n_dist, n_expand, n_dist_up, n_hops_up);
+    visit_end(vs);
     if constexpr (kStamp) {
       st[6] = __builtin_readcyclecounter() - t_begin;
       if (lane < 8) p.stamps[static_cast<uint64_t>(qi) * 8 + lane] = st[lane & 7];
@@ -410,11 +434,30 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
     wave_sync();
   }
 }
+// Roofline calibration (bench.py's measured peak): a streaming read of n16 16-byte words, four
+// independent dwordx4 loads in flight per lane per step, summed so the loads cannot be dropped.
+__global__ void __launch_bounds__(256) stream_read_kernel(const float4 *p, uint64_t n16, float *sink) {
+  float acc = 0.f;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const float4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+    acc += (a.x + b.x) + (c.x + d.x) + (a.w + b.w) + (c.w + d.w);
+  }
+  for (; i < n16; i += stride) acc += p[i].x;
+  if (acc == -1.2345f) *sink = acc;  // never true for the probe's zeroed buffer
+}
 }  // namespace
 
-size_t search_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool sq8, bool compact) {
+hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, float *sink, hipStream_t stream) {
+  hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const float4 *>(buf),
+                     bytes / 16, sink);
+  return hipGetLastError();
+}
+
+size_t search_wave_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact) {
   return static_cast<size_t>(stride) * 4 + 3 * 64 * 4 + 2 * (((ef + 1) * 4 + 15) / 16 * 16) +
-         visited_table_bytes(hash_log2, compact) + (sq8 ? 2 * static_cast<size_t>(stride) * 4 : 0);
+         visited_table_bytes(hash_log2, compact);
 }
 
 hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream) {
@@ -464,11 +507,11 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_or
   return ip ? kernel_ptr<true, 0>() : kernel_ptr<false, 0>();
 }
 
-hipError_t launch_search(const SearchParams &p, int grid, size_t lds, hipStream_t stream) {
+hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream) {
   const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
   SearchParams arg = p;
   void *args[] = {&arg};
-  return hipLaunchKernel(fn, dim3(grid), dim3(64), args, lds, stream);
+  return hipLaunchKernel(fn, dim3(grid), dim3(64 * waves), args, lds, stream);
 }
 
 hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint32_t n,
@@ -483,9 +526,9 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
   return hipGetLastError();
 }
 
-hipError_t search_occupancy(const SearchParams &p, size_t lds, int *blocks_per_cu) {
+hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu) {
   const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, lds);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * waves, lds);
 }
 
 }  // namespace alaya_amd
