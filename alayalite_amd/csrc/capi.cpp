@@ -212,12 +212,15 @@ int search_waves(const SearchParams &p) {
 }
 
 // Size the LDS visited table for residency: the batch wants ceil(nq / CUs) resident queries
-// (waves) per CU (capped by what the register file admits); the table takes what LDS is left per
-// wave, never more than ~2x the expected visited count (~24 ids per expansion x ef), never below
-// 1024 slots.  A query that outgrows its table spills to the global bitset (exact either way).
-// Layout: compact 16-bit slots (twice the entries per byte) whenever the ids' hash remainder fits
-// (log2 n - log2 slots <= 11), else 32-bit id slots.  A workgroup of W waves also holds the shared
-// region, counted per wave as shared / W.  Returns log2 slots; sets p.vis_*.
+// (waves) per CU; the register file caps that.  With more queries than resident slots the launch
+// runs as many waves as the registers admit -- a spill to the global second level is one atomicOr
+// per visit and no clearing beyond the words set (visit_end), so residency beats table size
+// (config 5, 10k queries: 4 -> 8 -> 12 waves per CU with 16 / 8 / 4 KB tables took 20.3 / 13.3 /
+// 11.1 ms; profiles/r03/sweeps) -- and the table takes what LDS is left per wave at that count
+// (workgroups of W waves plus the shared region), never below 1024 slots, never more than ~2x the
+// expected visited count (48 ef).  Layout: compact 16-bit slots (twice the entries per byte)
+// whenever the ids' hash remainder fits (log2 n - log2 slots <= 11), else 32-bit id slots.
+// Returns log2 slots; sets p.vis_*.
 constexpr uint32_t kMaxCompactRbits = 11;
 
 uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef, int W = 1) {
@@ -239,34 +242,23 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   }
   const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0);
   const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
-  const size_t fixed = wave_fixed + (shared + W - 1) / W;  // per wave
   int vgpr_blocks = 0;
   hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + 4096), &vgpr_blocks), "occupancy");
   const uint64_t vgpr_waves = static_cast<uint64_t>(std::max(1, vgpr_blocks)) * W;
   const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
   uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_waves, want));
   const uint32_t cap = ceil_log2(48ull * ef);
-  if (want > vgpr_waves) {
-    // Several queries per resident slot: residency beyond what keeps a table of ~32 ef slots
-    // (load <= ~0.5 at the usual 10-24 ef visited ids) costs more in probes and spills than it
-    // gains (SIFT 1M, 10k queries: 4 waves/SIMD with 8 KB tables beat 5 with 4 KB by ~20 %).
-    uint32_t tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(32ull * ef)));
-    if (const char *e = std::getenv("ALAYA_VISITED_TABLE_EF")) {  // diagnostics: slots per ef target
-      const uint64_t f = std::strtoull(e, nullptr, 10);
-      if (f) tl = std::max<uint32_t>(10, std::min<uint32_t>(16, ceil_log2(f * ef)));
-    }
-    auto per_wave = [&](uint32_t l) {
-      const bool tc = mode != 2 && fits_compact(l);
-      return fixed + (static_cast<size_t>(tc ? 2 : 4) << l);
-    };
-    // ... but never leave a SIMD without a wave for it: halve the table (down to ~16 ef slots)
-    // while fewer than one wave per SIMD would fit (10M x 768 SQ8 at ef 340: 32 KB tables admit
-    // 3 of the 4 waves the register file allows)
-    const uint64_t simd_floor = std::min<uint64_t>(4, vgpr_waves);
-    while (kLdsPerCu / per_wave(tl) < simd_floor && tl > 10 && (1ull << (tl - 1)) >= 16ull * ef) --tl;
-    waves = std::max<uint64_t>(1, std::min<uint64_t>(waves, kLdsPerCu / per_wave(tl)));
-  }
-  const size_t budget = kLdsPerCu / waves > fixed ? kLdsPerCu / waves - fixed : 0;
+  // table bytes per wave when `w` waves share a CU in workgroups of W
+  auto table_budget = [&](uint64_t w) -> size_t {
+    const uint64_t blocks = std::max<uint64_t>(1, w / W);
+    const size_t per_block = kLdsPerCu / blocks;
+    if (per_block <= shared) return 0;
+    const size_t per_wave = (per_block - shared) / W;
+    return per_wave > wave_fixed ? per_wave - wave_fixed : 0;
+  };
+  const size_t min_table = (mode == 2 || !fits_compact(10)) ? (4u << 10) : (2u << 10);
+  while (waves > static_cast<uint64_t>(W) && table_budget(waves) < min_table) waves -= W;
+  const size_t budget = table_budget(waves);
   auto pick = [&](size_t slot_bytes, uint32_t lmax) {
     uint32_t l = 10;
     while (l < lmax && (slot_bytes << (l + 1)) <= budget) ++l;

@@ -398,6 +398,13 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
   // chunk-major: a chunk's query / scale / min values feed every row slot, then die
 #pragma unroll
   for (int t = 0; t < kFull; ++t) {
+#ifndef ALAYA_SQ8_NO_FENCE
+    // keep the scheduler from hoisting later chunks' LDS reads (and their registers) above this
+    // chunk's FMAs: 199 -> 131 VGPRs at d = 768 (IP), i.e. 3 instead of 2 waves per SIMD (config
+    // 5 at 10k queries 12.2 -> 10.5 ms; with one row per lane group 123 VGPRs, but slower at 1k
+    // queries: profiles/r03/sweeps)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const int e = P * t + 4 * m;
     const float4 x = *reinterpret_cast<const float4 *>(xq + e);
     const float4 s = *reinterpret_cast<const float4 *>(sc + e);

@@ -1,0 +1,100 @@
+"""Launch-shape sweep of the graph search on a device-built graph: config 5 (sq8: 10M x 768 IP rows,
+workloads.datasets.text_like seeds 7/8, SQ8 search + reference rerank), config 3 (sift: 1M x 128 L2)
+or config 4 (gist: 1M x 960 L2), at a fixed ef over 10k (and 1k) queries, for each combination of
+searchers per workgroup (ALAYA_SEARCH_WAVES) and visited-table target (ALAYA_VISITED_TABLE_EF slots
+per ef; a negative value = a fixed log2 via set_hash_log2).  Prints the mean launch time, QPS, mean
+n_dist and a hash of the ids (equal hashes = identical results).
+
+usage: python tools/c5_sweep.py [--workload sq8] [--n 10000000] [--ef 340] [--waves 1,2,4] [--table 0,8,16,-12]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+if os.environ.get("ALAYA_AB_ROOT"):  # A/B: a saved build of the package (e.g. ab/base) instead of the tree's
+    sys.path.insert(0, os.environ["ALAYA_AB_ROOT"])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=("sq8", "sift", "gist"), default="sq8")
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--ef", type=int, default=0)
+    ap.add_argument("--nq", default="10000,1000")
+    ap.add_argument("--waves", default="0", help="searchers per workgroup; 0 = the engine's choice")
+    ap.add_argument("--table", default="0", help="slots per ef targets (0 = default policy); negative = fixed log2")
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from alayalite_amd import _native
+    import workloads.datasets as ds
+
+    ext = _native._ext
+    print("engine:", os.path.dirname(_native.__file__), flush=True)
+    gen, n0, ef0, metric, sq8 = {"sq8": (ds.text_like, 10_000_000, 340, 1, True),
+                                 "sift": (ds.sift_like, 1_000_000, 70, 0, False),
+                                 "gist": (ds.gist_like, 1_000_000, 387, 0, False)}[args.workload]
+    n, ef = args.n or n0, args.ef or ef0
+    t = time.time()
+    base, queries = gen(n, 10000)
+    print(f"data {base.shape} in {time.time() - t:.1f}s", flush=True)
+    dev = ext.DeviceIndex(0)
+    dev.set_base(base, metric)
+    t = time.time()
+    dev.build_graph(32, 100, 100, 0, 0, 2)
+    print(f"graph in {time.time() - t:.1f}s", flush=True)
+    if sq8:
+        mn, mx = ext.sq8_train(base)
+        dev.set_sq8(ext.sq8_encode(base, mn, mx, 16), mn, mx, ext.host_sq8_order())
+    del base
+    st = torch.cuda.current_stream()
+    for nq in [int(x) for x in args.nq.split(",")]:
+        qd = torch.from_numpy(np.ascontiguousarray(queries[:nq])).cuda()
+        ids = torch.empty((nq, 10), dtype=torch.int32, device="cuda")
+        dd = torch.empty((nq, 10), dtype=torch.float32, device="cuda")
+        cnt = torch.empty((nq, 4), dtype=torch.int32, device="cuda")
+        for w in args.waves.split(","):
+            os.environ.pop("ALAYA_SEARCH_WAVES", None)
+            if w != "0":
+                os.environ["ALAYA_SEARCH_WAVES"] = w
+            for tb in [int(x) for x in args.table.split(",")]:
+                os.environ.pop("ALAYA_VISITED_TABLE_EF", None)
+                dev.set_hash_log2(0)
+                if tb > 0:
+                    os.environ["ALAYA_VISITED_TABLE_EF"] = str(tb)
+                elif tb < 0:
+                    dev.set_hash_log2(-tb)
+
+                def run():
+                    if sq8:
+                        dev.search_sq8_device(qd.data_ptr(), 0, nq, 10, ef, 1, ids.data_ptr(), dd.data_ptr(),
+                                              cnt.data_ptr(), st.cuda_stream)
+                    else:
+                        dev.search_device(qd.data_ptr(), nq, 10, ef, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(),
+                                          st.cuda_stream)
+
+                for _ in range(2):
+                    run()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(args.reps):
+                    run()
+                e1.record(st)
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / args.reps
+                h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
+                c = cnt.cpu().numpy()
+                print(f"nq {nq} waves {w} table {tb}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
+                      f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}", flush=True)
+    os.environ.pop("ALAYA_SEARCH_WAVES", None)
+    os.environ.pop("ALAYA_VISITED_TABLE_EF", None)
+
+
+if __name__ == "__main__":
+    main()
