@@ -18,7 +18,10 @@ def _runtime_order():
     initialised first, then the engine's.  Loading the engine first left the engine with no device
     ("no HIP device available") once torch initialised afterwards (a GPU test run, r03), and
     initialising the engine first leaves torch without devices.  So when torch is importable it is
-    loaded and initialised here, before the extension."""
+    loaded and initialised here, before the extension (ALAYA_SKIP_TORCH_INIT=1 skips it for
+    processes that never use torch, e.g. the sanitizer driver)."""
+    if os.environ.get("ALAYA_SKIP_TORCH_INIT") == "1":
+        return
     try:
         import torch
     except ImportError:  # the engine itself does not need torch

@@ -1,11 +1,14 @@
 #!/bin/bash
 # ASAN and TSAN runs of the engine's host C++: the host translation units (capi.cpp,
 # hnsw_build.cpp, graph_update.cpp + the driver tools/sanitize/host_checks.cpp) are compiled with
-# -fsanitize=address / -fsanitize=thread; the HIP kernel objects are linked uninstrumented.  Logs go
-# to profiles/r02/sanitizers/.  CPU only.
+# -fsanitize=address / -fsanitize=thread; the HIP kernel objects are linked uninstrumented.  Then the
+# pybind module (pybind_module.cpp) under ASan: tools/build_pybind_asan.sh builds an instrumented copy
+# of the package and an ASan-linked embedded python, and tools/sanitize/pybind_driver.py runs its
+# host-only surface here (the Index API half runs on the GPU box: tools/run_pybind_asan_box.sh).
+# Logs go to profiles/r03/sanitizers/.  CPU only.
 set -euo pipefail
 cd "$(dirname "$0")/.."
-OUT=profiles/r02/sanitizers
+OUT=profiles/r03/sanitizers
 B=$(mktemp -d)
 mkdir -p "$OUT"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
@@ -34,3 +37,8 @@ for san in address thread; do
   fi
 done
 rm -rf "$B"
+bash tools/build_pybind_asan.sh > "$OUT/pybind_asan_build.log" 2>&1
+mkdir -p /tmp/pybind_asan_cpu
+ASAN_OPTIONS=detect_leaks=0:alloc_dealloc_mismatch=0:abort_on_error=1 sanitize_build/py_asan \
+  tools/sanitize/pybind_driver.py "$PWD/sanitize_build/pkg" /tmp/pybind_asan_cpu > "$OUT/pybind_asan_cpu.log" 2>&1 \
+  && echo "pybind asan (host surface): clean" || { echo "pybind asan: FAILED"; tail -30 "$OUT/pybind_asan_cpu.log"; exit 1; }
