@@ -217,7 +217,7 @@ int search_waves(const SearchParams &p) {
 // per visit and no clearing beyond the words set (visit_end), so residency beats table size
 // (config 5, 10k queries: 4 -> 8 -> 12 waves per CU with 16 / 8 / 4 KB tables took 20.3 / 13.3 /
 // 11.1 ms; profiles/r03/sweeps) -- and the table takes what LDS is left per wave at that count
-// (workgroups of W waves plus the shared region), never below 1024 slots, never more than ~2x the
+// (workgroups of W waves plus the shared region), never below 256 slots, never more than ~2x the
 // expected visited count (48 ef).  Layout: compact 16-bit slots (twice the entries per byte)
 // whenever the ids' hash remainder fits (log2 n - log2 slots <= 11), else 32-bit id slots.
 // Returns log2 slots; sets p.vis_*.
@@ -256,13 +256,13 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     const size_t per_wave = (per_block - shared) / W;
     return per_wave > wave_fixed ? per_wave - wave_fixed : 0;
   };
-  const size_t min_table = (mode == 2 || !fits_compact(10)) ? (4u << 10) : (2u << 10);
+  const size_t min_table = (mode == 2 || !fits_compact(9)) ? (4u << 8) : (2u << 9);  // 256 wide / 512 compact slots
   while (waves > static_cast<uint64_t>(W) && table_budget(waves) < min_table) waves -= W;
   const size_t budget = table_budget(waves);
   auto pick = [&](size_t slot_bytes, uint32_t lmax) {
-    uint32_t l = 10;
+    uint32_t l = 8;
     while (l < lmax && (slot_bytes << (l + 1)) <= budget) ++l;
-    return std::max<uint32_t>(10, std::min<uint32_t>(l, cap));
+    return std::max<uint32_t>(8, std::min<uint32_t>(l, cap));
   };
   if (mode == 0) {
     // a 32-bit id table of >= 32 ef slots (load <= ~0.3 at the usual 10-24 visited ids per ef)

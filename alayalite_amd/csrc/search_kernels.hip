@@ -22,6 +22,20 @@
 #include "search_kernels.h"
 #include "search_device.h"
 
+// Minimum waves per SIMD the compiler must leave room for, per search-kernel shape (the register
+// budget: 512 / waves VGPRs).  0 = no constraint.  Diagnostics builds override with
+// -DALAYA_MIN_WAVES_SQ8=... / -DALAYA_MIN_WAVES_NARROW=....
+#ifndef ALAYA_MIN_WAVES_SQ8
+#define ALAYA_MIN_WAVES_SQ8 0
+#endif
+#ifndef ALAYA_MIN_WAVES_NARROW
+#define ALAYA_MIN_WAVES_NARROW 0
+#endif
+template <int kChunks, int kSpace>
+constexpr int search_min_waves() {
+  return kSpace != 0 ? ALAYA_MIN_WAVES_SQ8 : (kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : 0);
+}
+
 namespace alaya_amd {
 
 namespace {
@@ -226,7 +240,9 @@ __device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, c
 // quantizer's scale / min); each wave is an independent persistent searcher with its own visited
 // spill slot.  After fill_shared the waves never synchronise again.
 template <bool kIP, int kChunks, bool kStamp, int kSpace = 0>
-__global__ void __launch_bounds__(256) hnsw_search_kernel(SearchParams p) {
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu(search_min_waves<kChunks, kSpace>() ? search_min_waves<kChunks, kSpace>() : 1,
+                                       8))) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = static_cast<int>(threadIdx.x >> 6);
