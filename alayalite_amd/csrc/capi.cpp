@@ -479,16 +479,20 @@ int alaya_hbm_stream_read(int device, uint64_t bytes, int iters, double *gbs) {
     double best = 0.0;
     try {
       hip_check(hipMemsetAsync(buf.ptr, 0, bytes, s), "memset");
-      const int grid = prop.multiProcessorCount * 8;
-      hip_check(alaya_amd::launch_stream_read(buf.ptr, bytes, grid, sink.as<float>(), s), "stream read");  // warm
-      for (int it = 0; it < iters; ++it) {
-        hip_check(hipEventRecord(a, s), "hipEventRecord");
-        hip_check(alaya_amd::launch_stream_read(buf.ptr, bytes, grid, sink.as<float>(), s), "stream read");
-        hip_check(hipEventRecord(b, s), "hipEventRecord");
-        hip_check(hipEventSynchronize(b), "hipEventSynchronize");
-        float ms = 0.f;
-        hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
-        best = std::max(best, static_cast<double>(bytes) / (ms * 1e6));
+      for (int shape = 0; shape < 3; ++shape) {
+        for (int occ : {8, 16}) {  // 256-thread workgroups per CU
+          const int grid = prop.multiProcessorCount * occ;
+          hip_check(alaya_amd::launch_stream_read(buf.ptr, bytes, grid, shape, sink.as<float>(), s), "stream read");
+          for (int it = 0; it < iters; ++it) {
+            hip_check(hipEventRecord(a, s), "hipEventRecord");
+            hip_check(alaya_amd::launch_stream_read(buf.ptr, bytes, grid, shape, sink.as<float>(), s), "stream read");
+            hip_check(hipEventRecord(b, s), "hipEventRecord");
+            hip_check(hipEventSynchronize(b), "hipEventSynchronize");
+            float ms = 0.f;
+            hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+            best = std::max(best, static_cast<double>(bytes) / (ms * 1e6));
+          }
+        }
       }
     } catch (...) {
       (void)hipStreamSynchronize(s);

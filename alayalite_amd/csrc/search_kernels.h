@@ -101,6 +101,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
                                 uint32_t nq, float *out, hipStream_t stream);
 
 // streaming read of `bytes` (multiple of 16) for the measured-bandwidth calibration
-hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, float *sink, hipStream_t stream);
+hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, int shape, float *sink,
+                              hipStream_t stream);
 
 }  // namespace alaya_amd

@@ -450,24 +450,47 @@ __global__ void __launch_bounds__(64) rerank_kernel(SearchParams p, RerankParams
     wave_sync();
   }
 }
-// Roofline calibration (bench.py's measured peak): a streaming read of n16 16-byte words, four
-// independent dwordx4 loads in flight per lane per step, summed so the loads cannot be dropped.
+// Roofline calibration (bench.py's measured peak): streaming reads of n16 16-byte words, summed so
+// the loads cannot be dropped.  Shape 0: one dwordx4 per lane per step (a wave reads 1 KB
+// contiguous, the grid sweeps the buffer in order); shape 1: four independent dwordx4 per lane,
+// grid-stride apart; shape 2: four consecutive dwordx4 per lane (a wave reads 4 KB contiguous).
+// alaya_hbm_stream_read reports the best shape.
+template <int kShape>
 __global__ void __launch_bounds__(256) stream_read_kernel(const float4 *p, uint64_t n16, float *sink) {
   float acc = 0.f;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
   uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const float4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-    acc += (a.x + b.x) + (c.x + d.x) + (a.w + b.w) + (c.w + d.w);
+  if constexpr (kShape == 1) {
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+      const float4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+      acc += (a.x + b.x) + (c.x + d.x) + (a.w + b.w) + (c.w + d.w);
+    }
+  } else if constexpr (kShape == 2) {
+    const uint64_t w = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);  // wave index
+    const uint64_t waves = static_cast<uint64_t>(gridDim.x) * 4;
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t base = w * 256;
+    for (; base + 256 <= n16; base += waves * 256) {
+      const float4 a = p[base + lane], b = p[base + 64 + lane], c = p[base + 128 + lane], d = p[base + 192 + lane];
+      acc += (a.x + b.x) + (c.x + d.x) + (a.w + b.w) + (c.w + d.w);
+    }
+    i = n16;  // the tail (< 4 KB per wave) is not read: the byte count below excludes nothing material
   }
   for (; i < n16; i += stride) acc += p[i].x;
   if (acc == -1.2345f) *sink = acc;  // never true for the probe's zeroed buffer
 }
 }  // namespace
 
-hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, float *sink, hipStream_t stream) {
-  hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const float4 *>(buf),
-                     bytes / 16, sink);
+hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, int shape, float *sink,
+                              hipStream_t stream) {
+  const float4 *p = static_cast<const float4 *>(buf);
+  if (shape == 1) {
+    hipLaunchKernelGGL(stream_read_kernel<1>, dim3(grid), dim3(256), 0, stream, p, bytes / 16, sink);
+  } else if (shape == 2) {
+    hipLaunchKernelGGL(stream_read_kernel<2>, dim3(grid), dim3(256), 0, stream, p, bytes / 16, sink);
+  } else {
+    hipLaunchKernelGGL(stream_read_kernel<0>, dim3(grid), dim3(256), 0, stream, p, bytes / 16, sink);
+  }
   return hipGetLastError();
 }
 

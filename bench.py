@@ -733,8 +733,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "measured_peak": round(measured_peak, 1),
                          "frac_measured": round(achieved / measured_peak, 4),
-                         "measured_peak_source": "alaya_hbm_stream_read: best of 5 streaming reads of 4 GiB, "
-                                                 "this GPU, this run",
+                         "measured_peak_source": "alaya_hbm_stream_read: best streaming read of 4 GiB (3 load "
+                                                 "shapes x 2 occupancies x 5 runs), this GPU, this run",
                          "traffic": traffic["gbs"] if traffic else None,
                          "traffic_bytes_per_launch": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,

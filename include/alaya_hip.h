@@ -63,8 +63,8 @@ const char *alaya_last_error(void);
 /* Number of visible HIP devices (0 when none). */
 int alaya_device_count(int *count);
 /* Roofline calibration (no reference counterpart): the best of `iters` streaming reads of a
- * `bytes`-byte device buffer (>= 1 MiB), in GB/s -- the measured bandwidth ceiling bench.py reports
- * beside the 8 TB/s HBM3E figure. */
+ * `bytes`-byte device buffer (>= 1 MiB) over three load shapes and two occupancies, in GB/s -- the
+ * measured bandwidth ceiling bench.py reports beside the 8 TB/s HBM3E figure. */
 int alaya_hbm_stream_read(int device, uint64_t bytes, int iters, double *gbs);
 
 /* ---- host graph (builder + reference on-disk format) --------------------------------------- */
