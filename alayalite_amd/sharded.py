@@ -65,9 +65,18 @@ def exchange_and_merge(local_ids, local_dists, offset: int, k: int, group=None):
     import torch
     import torch.distributed as dist
 
+    return exchange_packed(pack_candidates(to_global(local_ids, offset), local_dists), k, group)
+
+
+def exchange_packed(packed, k: int, group=None):
+    """The exchange of already packed keys (pack_candidates of global ids): one all_gather and the
+    merge sort; returns (ids, dists) on the keys' device.  With gloo on device tensors the keys go
+    through the host (copies only -- no device kernels between the copies)."""
+    import torch
+    import torch.distributed as dist
+
     world = dist.get_world_size(group)
-    device = local_ids.device
-    packed = pack_candidates(to_global(local_ids, offset), local_dists)
+    device = packed.device
     if dist.get_backend(group) == "gloo" and device.type != "cpu":  # gloo gathers host tensors
         packed = packed.cpu()
     parts = [torch.empty_like(packed) for _ in range(world)]
@@ -114,10 +123,14 @@ def shard_search(index, lo: int, sq8: bool, q_dev, k: int, ef: int, ids_dev, dis
 class ShardPipeline:
     """Double-buffered query batches (overlap the exchange with the next batch's search).
 
-    Batch i's search runs on the compute stream into buffer slot i % 2; its exchange (pack, one
-    all_gather, the merge sort) runs on a second stream once the search's event fires, while the
-    compute stream already searches batch i + 1.  The search of batch i + 2 reuses slot i % 2 only
-    after batch i's exchange has read it (an event the compute stream waits on).  The host issues
+    Batch i's search runs on the compute stream into buffer slot i % 2, followed there by the packing
+    of its (distance, global id) keys (a few elementwise kernels); its exchange (one all_gather, the
+    merge sort) runs on a second stream once the packing's event fires, while the compute stream
+    already searches batch i + 1.  Packing on the compute stream matters: the search kernel is
+    persistent and holds every CU slot it can, so a kernel queued on another stream behind it waits
+    for it to drain -- with gloo the exchange stream then carries only copies.  The exchange reads
+    only the packed keys, so slot i % 2's buffers are free for batch i + 2 once the compute stream
+    has packed them (stream order).  The host issues
     search i + 1 before exchange i, so a blocking exchange (gloo with host copies) still overlaps the
     device search.  On CPU tensors (gloo tests) the same loop runs without streams.
 
@@ -132,13 +145,12 @@ class ShardPipeline:
         mk = lambda dt, w: torch.empty((nq, w), dtype=dt, device=self.device)  # noqa: E731
         self.bufs = [(mk(torch.int32, k), mk(torch.float32, k), mk(torch.int32, 4)) for _ in range(2)]
         self.rows = [0, 0]
+        self.packed = [None, None]  # packed keys of the batch in each slot (compute stream)
         self.gpu = self.device.type == "cuda"
         if self.gpu:
             self.compute = torch.cuda.Stream(self.device)
             self.exch = torch.cuda.Stream(self.device)
             self.searched = [torch.cuda.Event() for _ in range(2)]
-            self.exchanged = [torch.cuda.Event() for _ in range(2)]
-            self.used = [False, False]
         self.timing = timing and self.gpu
         self.spans = []  # (start, end) events around each search on the compute stream (timing=True)
 
@@ -152,10 +164,9 @@ class ShardPipeline:
         if not self.gpu:
             self.search_fn(q, ids, d, c, 0)
             return
-        if self.used[slot]:
-            self.compute.wait_event(self.exchanged[slot])
+        import torch
+
         if self.timing:
-            import torch
 
             span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             span[0].record(self.compute)
@@ -163,8 +174,9 @@ class ShardPipeline:
         if self.timing:
             span[1].record(self.compute)
             self.spans.append(span)
+        with torch.cuda.stream(self.compute):
+            self.packed[slot] = pack_candidates(to_global(ids, self.offset), d)
         self.searched[slot].record(self.compute)
-        self.used[slot] = True
 
     def _exchange(self, slot):
         import torch
@@ -174,8 +186,9 @@ class ShardPipeline:
             return exchange_and_merge(ids, d, self.offset, self.k, self.group)
         with torch.cuda.stream(self.exch):
             self.exch.wait_event(self.searched[slot])
-            out = exchange_and_merge(ids, d, self.offset, self.k, self.group)
-            self.exchanged[slot].record(self.exch)
+            packed = self.packed[slot]
+            packed.record_stream(self.exch)
+            out = exchange_packed(packed, self.k, self.group)
         return out
 
     def run(self, batches):
