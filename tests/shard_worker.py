@@ -1,7 +1,8 @@
 """One rank of the sharded-search GPU test (tests/test_shard_gpu.py), started as a child process.
 
 Every rank runs on cuda:0 with a gloo group (a one-GPU box rehearses the N-GPU path; bench.py runs
-the same ShardedIndex / exchange_and_merge code over RCCL).  The rank builds its shard's graph on
+the same ShardedIndex / exchange_and_merge code over RCCL), or, with ALAYA_TEST_BACKEND=nccl, as a
+single rank over RCCL itself.  The rank builds its shard's graph on
 the host, searches the queries on the device (ShardedIndex.search: shard_search_device + the
 all_gather exchange + merge, on device tensors), and writes the merged result plus the oracle's
 search of its own shard (the restatement of search_solo on the shard's graph) for rank 0 to check.
@@ -59,7 +60,12 @@ def main():
     from alayalite_amd.sharded import EMPTY, ShardedIndex
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo")
+    # ALAYA_TEST_BACKEND=nccl: RCCL on cuda:0 (one rank per GPU -- a one-GPU box runs world 1), the
+    # device-tensor all_gather bench.py uses on a node; default gloo (several ranks on one GPU)
+    if os.environ.get("ALAYA_TEST_BACKEND", "gloo") == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
     base, queries = _data(mode, n, dim, nq, seed)
     metric = 1 if mode == "sq8" else 0
 
