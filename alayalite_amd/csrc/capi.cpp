@@ -222,6 +222,16 @@ int search_waves(const SearchParams &p) {
 // whenever the ids' hash remainder fits (log2 n - log2 slots <= 11), else 32-bit id slots.
 // Returns log2 slots; sets p.vis_*.
 constexpr uint32_t kMaxCompactRbits = 11;
+// At most 4 searchers per SIMD: a 5th wave (the 96-VGPR d = 128 L2 kernel admits 5) halves every
+// table and costs more in probes than it hides -- SIFT 1M, 10k queries, ef 70: 16 waves per CU with
+// 4096-slot tables 1.198 ms, 20 with 2048-slot tables 1.513 ms (profiles/r03/sweeps/sift_max_waves.log);
+// config 5 measured 12 and 16 per CU equal.
+constexpr uint64_t kMaxSearchWavesPerCu = 16;
+uint64_t max_search_waves_per_cu() {
+  if (const char *e = std::getenv("ALAYA_MAX_WAVES_PER_CU"))  // diagnostics (tools/shape_sweep.py)
+    return std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  return kMaxSearchWavesPerCu;
+}
 
 uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef, int W = 1) {
   const uint32_t lbits = std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2)));
@@ -246,7 +256,8 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + 4096), &vgpr_blocks), "occupancy");
   const uint64_t vgpr_waves = static_cast<uint64_t>(std::max(1, vgpr_blocks)) * W;
   const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
-  uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>(vgpr_waves, want));
+  const uint64_t max_waves = std::max<uint64_t>(W, max_search_waves_per_cu());
+  uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>({vgpr_waves, want, max_waves}));
   const uint32_t cap = ceil_log2(48ull * ef);
   // table bytes per wave when `w` waves share a CU in workgroups of W
   auto table_budget = [&](uint64_t w) -> size_t {
@@ -326,7 +337,7 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   if (lds > kLdsPerCu) throw ArgError("ef / dim too large for the LDS budget");
   int per_cu = 0;
   hip_check(alaya_amd::search_occupancy(p, W, lds, &per_cu), "occupancy");
-  per_cu = std::max(1, per_cu);
+  per_cu = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(per_cu, max_search_waves_per_cu() / W)));
   const uint64_t blocks_needed = (nq + W - 1) / W;
   const uint64_t grid64 = std::min<uint64_t>(blocks_needed, static_cast<uint64_t>(per_cu) * ix->num_cus);
   const int grid = static_cast<int>(std::max<uint64_t>(1, grid64));

@@ -36,10 +36,12 @@ template <int kXor>
 __device__ __forceinline__ float lane_xor(float v) {
   const int x = __builtin_bit_cast(int, v);
   int r;
+  // quad permutes read a lane of the same quad, so every lane is written: no "old" operand (a
+  // zeroed register per move with update_dpp(0, ...))
   if constexpr (kXor == 1) {
-    r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    r = __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
   } else if constexpr (kXor == 2) {
-    r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    r = __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
   } else {
     static_assert(kXor == 4 || kXor == 8 || kXor == 16, "lane_xor: 1, 2, 4, 8 or 16");
     r = __builtin_amdgcn_ds_swizzle(x, (kXor << 10) | 0x1F);        // and 0x1f, xor kXor
@@ -125,9 +127,14 @@ __device__ __forceinline__ float finish_tail(const SearchParams &p, const float 
 // within ~96 float4 (384 VGPRs) -- one wave per SIMD has the whole 512-entry register file.
 // Small rows (d <= 256): 2 rows per group = 16 rows per pass, which covers the ~10 fresh
 // neighbours of a typical expansion in one pass and leaves registers for more resident waves.
+#ifndef ALAYA_NARROW_RPL
+#define ALAYA_NARROW_RPL 2  // diagnostics builds: -DALAYA_NARROW_RPL=1 (8-row passes, fewer VGPRs)
+#endif
 template <int kChunks>
 constexpr int rows_per_group() {
-  return kChunks <= 0 ? 1 : kChunks <= 8 ? 2 : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
+  return kChunks <= 0 ? 1
+         : kChunks <= 8 ? ALAYA_NARROW_RPL
+                        : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
 }
 
 // One pass of row loads in registers: lane group g (8 lanes) takes rows base + g + 8r, r < kR.
@@ -159,51 +166,49 @@ __device__ __forceinline__ void issue_rows(const SearchParams &p, const uint32_t
 #pragma unroll
   for (int r = 0; r < kRPL; ++r) {
     const float4 *rp = reinterpret_cast<const float4 *>(p.base + static_cast<uint64_t>(P.id[r]) * p.stride) + m;
-    if (base + 8 * r < n) {  // wave-uniform
+    if (base + 8 * r < n) {  // wave-uniform; a skipped slot is never read (finish_rows' `live`)
 #pragma unroll
       for (int t = 0; t < kChunks; ++t) P.y[r][t] = rp[8 * t];
-    } else {
-#pragma unroll
-      for (int t = 0; t < kChunks; ++t) P.y[r][t] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
 
-// Distances of an issued pass -> out[base + g + 8r].
+// Distances of an issued pass -> out[base + g + 8r].  The kChunks > 0 kernels run only for
+// dim == 32 * kChunks (search_kernel_symbol / the build's dispatch pick them from dim % 32 == 0), so
+// there is no 8-block or scalar tail.  Row slots past n (wave-uniform) are skipped whole.
 template <bool kIP, int kChunks>
-__device__ __forceinline__ void finish_rows(const SearchParams &p, const float *q, int base,
+__device__ __forceinline__ void finish_rows(const SearchParams &p, const float *q, int n, int base,
                                             RowPass<kChunks> &P, float *out) {
   constexpr int kRPL = RowPass<kChunks>::kR;
   const int lane = lane_id();
   const int g = lane >> 3, m = lane & 7;
-  constexpr int T = kChunks;
-  const int rem = static_cast<int>(p.dim) - 32 * T;
-  const int nb8 = rem >> 3;
-  const int tail_begin = 32 * T + 8 * nb8;
+  int live = 0;  // wave-uniform number of row slots in use
   float a[kRPL][4];
 #pragma unroll
-  for (int r = 0; r < kRPL; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
+  for (int r = 0; r < kRPL; ++r) {
+    a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.f;
+    live += base + 8 * r < n ? 1 : 0;
+  }
   const float4 *qp = reinterpret_cast<const float4 *>(q) + m;
 #pragma unroll
   for (int t = 0; t < kChunks; ++t) {
     const float4 x = qp[8 * t];
 #pragma unroll
-    for (int r = 0; r < kRPL; ++r) accumulate<kIP>(x, P.y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
+    for (int r = 0; r < kRPL; ++r) {
+      if (r >= live) break;
+      accumulate<kIP>(x, P.y[r][t], a[r][0], a[r][1], a[r][2], a[r][3]);
+    }
   }
 #pragma unroll
   for (int r = 0; r < kRPL; ++r) {
-    const float *row = p.base + static_cast<uint64_t>(P.id[r]) * p.stride;
-    if (m < 2) {  // trailing 8-element blocks feed acc[0..7] (lanes m = 0, 1)
-      for (int b = 0; b < nb8; ++b) {
-        const int e = 32 * T + 8 * b + 4 * m;
-        if (P.act[r]) {
-          accumulate<kIP>(*reinterpret_cast<const float4 *>(q + e),
-                          *reinterpret_cast<const float4 *>(row + e), a[r][0], a[r][1], a[r][2], a[r][3]);
-        }
-      }
+    if (r >= live) break;
+    float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
+    if (P.act[r] && m == 0) {
+      if (kIP) res = -res;
+      const uint32_t id = P.id[r];
+      if (p.valid != nullptr && !((p.valid[id >> 5] >> (id & 31)) & 1u)) res = FLT_MAX;
+      out[base + g + 8 * r] = res;
     }
-    const float res = finish_row<kIP>(a[r][0], a[r][1], a[r][2], a[r][3]);
-    if (P.act[r] && m == 0) out[base + g + 8 * r] = finish_tail<kIP>(p, q, row, tail_begin, res, P.id[r]);
   }
 }
 
@@ -258,7 +263,7 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
     for (int base = 0; base < n; base += kStep) {
       RowPass<kChunks> P;
       issue_rows<kChunks>(p, ids, n, base, P);
-      finish_rows<kIP, kChunks>(p, q, base, P, out);
+      finish_rows<kIP, kChunks>(p, q, n, base, P, out);
     }
     (void)g; (void)m; (void)tail_begin;
   } else {
@@ -385,8 +390,13 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
   constexpr int P = SP::P, LPR = SP::LPR, G = SP::G;
   const int lane = lane_id();
   const int g = lane / LPR, m = lane % LPR;
-  const int rem = static_cast<int>(p.dim) - P * kFull;
-  const bool half = rem >= P / 2;
+  // kFull > 0 kernels run only for dim == P * kFull (dim / 32 chunks of 32 codes, or twice as many
+  // of 16), so rem == 0: no half block, no scalar tail.  The AVX-512 order drops the dead tail code;
+  // the AVX2 order keeps it, because without it the compiler schedules the 48-chunk loop into
+  // 186-235 VGPRs (2 waves per SIMD) instead of 121-144.
+  constexpr bool kTail = kOrder == 1;
+  const int rem = kTail ? static_cast<int>(p.dim) - P * kFull : 0;
+  const bool half = kTail && rem >= P / 2;
   const int tail_begin = P * kFull + (half ? P / 2 : 0);
   float acc[SP::kR][4];
   int live = 0;  // wave-uniform number of row slots in use
@@ -423,7 +433,7 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
   }
 #pragma unroll
   for (int r = 0; r < SP::kR; ++r) {
-    if (base + G * r >= n) break;
+    if (r >= live) break;
     const uint8_t *rw = p.codes + static_cast<uint64_t>(S.id[r]) * p.code_stride;
     if (half && m < LPR / 2 && S.act[r])  // trailing half block -> acc[0 .. P/2)
       sq8_chunk<kIP>(xq, sc, mnv, P * kFull + 4 * m, *reinterpret_cast<const uint32_t *>(rw + P * kFull + 4 * m),
@@ -436,8 +446,10 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
     a0 += lane_xor<1>(a0); a1 += lane_xor<1>(a1); a2 += lane_xor<1>(a2); a3 += lane_xor<1>(a3);
     float res = kOrder == 2 ? (a0 + a2) + (a1 + a3) : (a0 + a1) + (a2 + a3);
     if (S.act[r] && m == 0) {
-      for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
-        res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(rw[e]), res);
+      if constexpr (kTail) {
+        for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
+          res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(rw[e]), res);
+      }
       out[base + g + G * r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
     }
   }

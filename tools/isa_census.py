@@ -177,7 +177,7 @@ def main() -> None:
         r.update(resource_comments(asm, name))
         rows.append(r)
     for r in rows:
-        print(f"{r['kernel']:<44} sgpr {r.get('TotalNumSgprs', '?'):>3} vgpr {r.get('NumVgprs', '?'):>3} "
+        print(f"{r['kernel']:<44} scratch {r.get('ScratchSize', '?'):>3} sgpr {r.get('TotalNumSgprs', '?'):>3} vgpr {r.get('NumVgprs', '?'):>3} "
               f"occ {r.get('Occupancy', '?')}  spill slots {r['spill_slots']:>2}  restores {r['restores_total']:>3} "
               f"(in expansion loops: {r['restores_in_expansion_loops']}; loops {len(r['expansion_loops'])}, "
               f"insts {sum(v['insts'] for v in r['expansion_loops'].values())})")

@@ -1,11 +1,11 @@
 """Launch-shape sweep of the graph search on a device-built graph: config 5 (sq8: 10M x 768 IP rows,
 workloads.datasets.text_like seeds 7/8, SQ8 search + reference rerank), config 3 (sift: 1M x 128 L2)
 or config 4 (gist: 1M x 960 L2), at a fixed ef over 10k (and 1k) queries, for each combination of
-searchers per workgroup (ALAYA_SEARCH_WAVES) and visited-table target (ALAYA_VISITED_TABLE_EF slots
-per ef; a negative value = a fixed log2 via set_hash_log2).  Prints the mean launch time, QPS, mean
+searchers per workgroup (ALAYA_SEARCH_WAVES), cap on resident searchers per CU
+(ALAYA_MAX_WAVES_PER_CU) and visited table (a negative value = a fixed log2 via set_hash_log2).  Prints the mean launch time, QPS, mean
 n_dist and a hash of the ids (equal hashes = identical results).
 
-usage: python tools/c5_sweep.py [--workload sq8] [--n 10000000] [--ef 340] [--waves 1,2,4] [--table 0,8,16,-12]
+usage: python tools/shape_sweep.py [--workload sq8] [--n 10000000] [--ef 340] [--waves 1,2,4] [--max-waves 0,12,16] [--table 0,-12]
 """
 import argparse
 import os
@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--ef", type=int, default=0)
     ap.add_argument("--nq", default="10000,1000")
     ap.add_argument("--waves", default="0", help="searchers per workgroup; 0 = the engine's choice")
+    ap.add_argument("--visited", default="0", help="visited-table layouts: 0 auto, 1 compact, 2 wide")
+    ap.add_argument("--max-waves", default="0", help="caps on resident searchers per CU (ALAYA_MAX_WAVES_PER_CU); 0 = none")
     ap.add_argument("--table", default="0", help="slots per ef targets (0 = default policy); negative = fixed log2")
     ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
@@ -59,10 +61,15 @@ def main():
         ids = torch.empty((nq, 10), dtype=torch.int32, device="cuda")
         dd = torch.empty((nq, 10), dtype=torch.float32, device="cuda")
         cnt = torch.empty((nq, 4), dtype=torch.int32, device="cuda")
-        for w in args.waves.split(","):
+        for w, mw, vm in [(w, mw, vm) for w in args.waves.split(",") for mw in args.max_waves.split(",")
+                          for vm in args.visited.split(",")]:
+            dev.set_visited_mode(int(vm))
             os.environ.pop("ALAYA_SEARCH_WAVES", None)
             if w != "0":
                 os.environ["ALAYA_SEARCH_WAVES"] = w
+            os.environ.pop("ALAYA_MAX_WAVES_PER_CU", None)
+            if mw != "0":
+                os.environ["ALAYA_MAX_WAVES_PER_CU"] = mw
             for tb in [int(x) for x in args.table.split(",")]:
                 os.environ.pop("ALAYA_VISITED_TABLE_EF", None)
                 dev.set_hash_log2(0)
@@ -90,10 +97,10 @@ def main():
                 ms = e0.elapsed_time(e1) / args.reps
                 h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
                 c = cnt.cpu().numpy()
-                print(f"nq {nq} waves {w} table {tb}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
+                print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
                       f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}", flush=True)
     os.environ.pop("ALAYA_SEARCH_WAVES", None)
-    os.environ.pop("ALAYA_VISITED_TABLE_EF", None)
+    os.environ.pop("ALAYA_MAX_WAVES_PER_CU", None)
 
 
 if __name__ == "__main__":
