@@ -1,8 +1,13 @@
 #!/bin/bash
-# one GPU call: SIFT 10k visited-table layouts / sizes at the default residency, SQ counters of
-# config 5 at 10k queries (tools/run_pmc_sq.sh)
+# one GPU call: parity suite on the tree, then tree vs ab/slot (slot-at-a-time visited probes)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 source tools/gpu_steps.sh
-step 300 gpurun_out/sw_sift_visited.log python -u tools/shape_sweep.py --workload sift --nq 10000 --visited 0,1,2 --table 0,-11,-13
-WORKLOAD=sq8 NQ=10000 EF=340 bash tools/run_pmc_sq.sh
+step 600 gpurun_out/gpu_suite.log python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread
+grep -q " passed" gpurun_out/gpu_suite.log && ! grep -q " failed" gpurun_out/gpu_suite.log || exit 1
+for v in tree slot; do
+  if [ "$v" = tree ]; then unset ALAYA_AB_ROOT; else export ALAYA_AB_ROOT=$GRAFT_REPO_ROOT/ab/$v; fi
+  step 300 gpurun_out/grp_sift_$v.log python -u tools/shape_sweep.py --workload sift --nq 10000,1000 --visited 0,1
+  step 300 gpurun_out/grp_gist_$v.log python -u tools/shape_sweep.py --workload gist --nq 1000
+  step 500 gpurun_out/grp_sq8_$v.log python -u tools/shape_sweep.py --workload sq8 --nq 10000,1000
+done
