@@ -1,0 +1,58 @@
+"""ISA guards on the search kernels (CPU-only: hipcc cross-compiles gfx950 to assembly here).
+
+tools/isa_census.py finds each hnsw_search_kernel instantiation's expansion loops (the depth-2 loops
+that probe the LDS visited table and gather rows) and counts SGPR spill restores inside them.  A
+restore there runs once per expansion; round 3 took the d = 960 kernel (the headline) from 108 to 0
+and the d = 128 kernel from 2 to 0.  These tests keep it that way, and keep the
+register budgets the residency policy was measured with."""
+
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+pytestmark = pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") and not shutil.which("hipcc"),
+                                reason="needs hipcc to compile the kernels to assembly")
+
+
+@pytest.fixture(scope="module")
+def census():
+    import isa_census as ic
+
+    asm = ic.compile_asm(ic.SRC, [])
+    rows = {}
+    for name, body in ic.split_functions(asm).items():
+        if "hnsw_search_kernel" in name:
+            r = ic.census(name, body)
+            r.update(ic.resource_comments(asm, name))
+            rows[r["kernel"]] = r
+    return rows
+
+
+@pytest.mark.parametrize("chunks", [4, 8, 16, 24, 30, 32])
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+def test_fixed_d_f32_expansion_loops_restore_no_spilled_sgpr(census, metric, chunks):
+    r = census[f"{metric} chunks={chunks} stamp=0 space=f32"]
+    assert r["expansion_loops"], "no expansion loop found"
+    assert r["restores_in_expansion_loops"] == 0, r["expansion_loops"]
+
+
+@pytest.mark.parametrize("space", ["sq8-avx512", "sq8-avx2"])
+@pytest.mark.parametrize("chunks", [4, 24, 30])
+def test_sq8_expansion_loops_restore_no_spilled_sgpr(census, space, chunks):
+    r = census[f"ip chunks={chunks} stamp=0 space={space}"]
+    assert r["restores_in_expansion_loops"] == 0, r["expansion_loops"]
+
+
+def test_register_budgets(census):
+    # no scratch in any search kernel; the 768-d AVX-512 SQ8 IP kernel (config 5) fits 4 waves per
+    # SIMD; the d = 128 kernels stay at >= 4 waves per SIMD (the residency cap is 4)
+    for k, r in census.items():
+        assert r.get("ScratchSize", 0) == 0, k
+    assert census["ip chunks=24 stamp=0 space=sq8-avx512"]["NumVgprs"] <= 128
+    for m in ("l2", "ip"):
+        assert census[f"{m} chunks=4 stamp=0 space=f32"]["Occupancy"] >= 4
