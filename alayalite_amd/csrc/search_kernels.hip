@@ -134,6 +134,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
   if (p.levels != nullptr) {
     // OverlayGraph::initialize (overlay_graph.hpp:122-144): greedy descent, strict '<'.
     uint32_t u = p.ep;
+    uint64_t off_u = p.upper_off[u];  // u's upper-level lists, kept while u stays
     if (lane == 0) L.cid[0] = u;
     wave_sync();
     space_distances<kIP, kChunks, kSpace>(p, L, L.cid, 1, L.cd);
@@ -143,27 +144,38 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
       bool changed = true;
       while (changed) {
         changed = false;
-        const uint32_t *list = p.upper_edges + p.upper_off[u] +
-                               static_cast<uint64_t>(level - 1) * p.upper_R;
+        const uint32_t *list = p.upper_edges + off_u + static_cast<uint64_t>(level - 1) * p.upper_R;
         const uint32_t v = lane < static_cast<int>(p.upper_R) ? list[lane] : kEmpty;
         const uint64_t endm = ballot(lane < static_cast<int>(p.upper_R) && v == kEmpty);
         const int cnt = endm ? __ffsll(static_cast<unsigned long long>(endm)) - 1
                              : static_cast<int>(p.upper_R);
         ++n_hops_up;
+        const bool has = lane < cnt;
+        // every candidate's list offset is loaded beside its row: the hop to the winner then needs
+        // one dependent load (its list), not two
+        uint64_t off_v = 0;
+        if (has) off_v = p.upper_off[v];
         wave_sync();
-        if (lane < cnt) L.cid[lane] = v;
+        if (has) L.cid[lane] = v;
         wave_sync();
         space_distances<kIP, kChunks, kSpace>(p, L, L.cid, cnt, L.cd);
         n_dist_up += cnt;
-        // first index of the minimum == the sequential strict-'<' scan's final choice
-        float dl = lane < cnt ? L.cd[lane] : FLT_MAX;
-        bool has = lane < cnt;
-        float mn = has ? dl : FLT_MAX;
-        for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+        // first index of the minimum == the sequential strict-'<' scan's final choice (the minimum
+        // is order-free: DPP / swizzle steps within each 32-lane half, then the two halves)
+        const float dl = has ? L.cd[lane] : FLT_MAX;
+        float mn = dl;
+        mn = fminf(mn, lane_xor<1>(mn));
+        mn = fminf(mn, lane_xor<2>(mn));
+        mn = fminf(mn, lane_xor<4>(mn));
+        mn = fminf(mn, lane_xor<8>(mn));
+        mn = fminf(mn, lane_xor<16>(mn));
+        mn = fminf(read_lane(mn, 0), read_lane(mn, 32));
         const uint64_t at = ballot(has && dl == mn);
         if (at && mn < cur) {
           const int w = __ffsll(static_cast<unsigned long long>(at)) - 1;
           u = read_lane(v, w);
+          off_u = (static_cast<uint64_t>(read_lane(static_cast<uint32_t>(off_v >> 32), w)) << 32) |
+                  read_lane(static_cast<uint32_t>(off_v), w);
           cur = mn;
           changed = true;
         }
