@@ -241,6 +241,14 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     p.vis_rbits = compact ? (lbits > l ? lbits - l : 0u) : alaya_amd::kVisWide;
     p.vis_max_disp = compact ? (0xffffu >> p.vis_rbits) - 1u : 0u;
     if (compact && mode == 3) p.vis_max_disp = std::min<uint32_t>(p.vis_max_disp, 2u);
+    p.vis_limit = 0u;
+    if (const char *e = std::getenv("ALAYA_VIS_LIMIT_PCT")) {  // diagnostics: spill threshold in % of slots
+      const uint64_t slots = 1ull << l;
+      const uint64_t lim = slots * std::min<uint64_t>(100, std::strtoull(e, nullptr, 10)) / 100;
+      // exact at any threshold up to slots - 64: one visit inserts at most 64 ids, and a compact
+      // probe past max_disp spills by itself
+      p.vis_limit = static_cast<uint32_t>(std::max<uint64_t>(64, std::min<uint64_t>(lim, slots - 64)));
+    }
     return l;
   };
   auto fits_compact = [&](uint32_t l) { return (lbits > l ? lbits - l : 0u) <= kMaxCompactRbits; };
@@ -1149,6 +1157,7 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
       bp.s.vis_rbits = probe.vis_rbits;
       bp.s.vis_lbits = probe.vis_lbits;
       bp.s.vis_max_disp = probe.vis_max_disp;
+      bp.s.vis_limit = probe.vis_limit;
       if (lds > kLdsPerCu) throw ArgError("ef_construction / dim too large for the LDS budget");
     }
     const size_t lds = alaya_amd::build_lds_bytes(ix->stride, ef, bp.s.hash_log2, bp.s.vis_rbits != alaya_amd::kVisWide);

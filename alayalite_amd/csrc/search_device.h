@@ -607,6 +607,7 @@ __device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t 
     vs.lshift = p.vis_lbits < p.hash_log2 ? p.hash_log2 - p.vis_lbits : 0u;
     vs.max_disp = p.vis_max_disp;
   }
+  if (p.vis_limit != 0u) vs.limit = p.vis_limit;
   return vs;
 }
 

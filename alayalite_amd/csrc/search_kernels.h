@@ -53,6 +53,8 @@ struct SearchParams {
   uint32_t vis_rbits;
   uint32_t vis_lbits;
   uint32_t vis_max_disp;  // compact: largest probe distance an entry may sit at (<= 0xffff >> rbits - 1)
+  uint32_t vis_limit;     // LDS table entries before a query spills to the second level (0 = the
+                          // layout's default: half the slots wide, 11/16 compact); <= slots - 64
   uint64_t *stamps;       // nullable: diagnostic per-phase cycle counts, nq x 8
   // SQ8 search space (SQ8Space, space/sq8_space.hpp): traversal distances on uint8 codes
   int sq8_order;          // 0 = f32 RawSpace search; 2 = AVX-512 SQ8 order; 1 = AVX2 SQ8 order
