@@ -106,3 +106,24 @@ def test_sq8_searchers_per_workgroup(native, orc, monkeypatch, waves, nq):
     dev.set_sq8(codes, mn, mx, 2)
     ids, d, c = dev.search_sq8(queries, 10, 64, 0)
     _check(view, ids, d, c, queries, 10, 64)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("pct", ["50", "95", "100"])
+def test_spill_threshold_keeps_results_exact(native, orc, monkeypatch, mode, pct):
+    """The first-level spill threshold (ALAYA_VIS_LIMIT_PCT, clamped to slots - 64) only moves the
+    point where a query starts using the second level: compact and wide 256-slot tables filled to
+    any threshold return the restatement's ids, distance bits and counters."""
+    monkeypatch.setenv("ALAYA_VIS_LIMIT_PCT", pct)
+    rng = np.random.default_rng(41)
+    base = rng.random((6000, 24), dtype=np.float32)
+    queries = rng.random((80, 24), dtype=np.float32)
+    g = native.Graph.build(base, 0, 32, 100, 8, 100)
+    l0, levels, off, ue, ep, upper_r, _ = g.arrays()
+    view = orc.IndexView(base, l0, levels, off, ue, upper_r, ep)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    dev.set_graph(g)
+    dev.set_hash_log2(8)
+    dev.set_visited_mode(mode)
+    _check(view, *dev.search(queries, 10, 150), queries, 10, 150)
