@@ -681,7 +681,12 @@ __device__ __forceinline__ int table_insert(const Visited &vs, uint32_t v) {
 __device__ __forceinline__ void spill_begin(Visited &vs) { vs.spilled = true; }
 
 // All lanes with `act` insert their v; duplicates among lanes must have been removed.
-__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
+// pre_ok (wave-uniform): pre_w holds, per lane, the current value of the second-level word of this
+// lane's v (spill_prefetch below, issued for exactly this adjacency row after the previous expansion's
+// visits had completed; the wave is the slot's only writer and nothing is visited in between).  A set
+// bit then means visited without a round trip, and a clear one means fresh unless the (read-only)
+// first level holds v: its bit is set by an atomic whose result nobody waits for.
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, bool pre_ok, uint32_t pre_w) {
   bool fresh = false;
   bool global = false;
   if (!vs.spilled) {
@@ -694,12 +699,16 @@ __device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
       global = r == 2;
     }
   } else if (act) {
-    global = !table_lookup(vs, v);
+    global = !(pre_ok && ((pre_w >> (v & 31)) & 1u)) && !table_lookup(vs, v);
   }
   if (vs.spilled) {  // wave-uniform
     const uint32_t bit = 1u << (v & 31);
     uint32_t old = bit;
-    if (global) {
+    if (global && pre_ok) {
+      __hip_atomic_fetch_or(&vs.bits[v >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = pre_w;  // exact: the word as it is now (two lanes of one word may both see it empty;
+      fresh = true; // the dirty list then names the word twice, which only clears it twice)
+    } else if (global) {
       old = atomicOr(&vs.bits[v >> 5], bit);
       fresh = (old & bit) == 0u;
     }
@@ -714,6 +723,19 @@ __device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
     }
   }
   return fresh;
+}
+
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) { return visit(vs, v, act, false, 0u); }
+
+// After an expansion's distances (its visits are complete: the wave waited for its row loads, which
+// were issued after them), read the second-level words of the predicted next expansion's adjacency
+// row (`row`, lane-aligned as the next visit will see it).  The load is agent-scope so it reads L2,
+// where the wave's own atomics landed, not a stale vector-L1 copy.  Used only if the prediction holds.
+__device__ __forceinline__ uint32_t spill_prefetch(const Visited &vs, uint32_t row_v, bool lane_in_row) {
+  uint32_t w = 0u;
+  if (lane_in_row && row_v != kEmpty)
+    w = __hip_atomic_load(&vs.bits[row_v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return w;
 }
 
 // End of a query: leave the slot's bitset clean for the next one (the words on the dirty list, or

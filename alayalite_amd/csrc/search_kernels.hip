@@ -292,6 +292,12 @@ __global__ void __launch_bounds__(256)
     // expansion unless the merge puts a closer candidate in front of it.  Its 128 B row is loaded
     // into registers while this expansion runs and used only if the next pop returns that id.
     uint32_t pred = kEmpty, pred_v = kEmpty;
+    // Second-level visited words of the predicted next expansion (spilled queries, spill_prefetch):
+    // the SQ8 kernels only, where config 5's 10k-query batch spills almost every query (its 10M ids
+    // fit only a few hundred LDS slots at full residency): 10.43 -> 9.76 ms.  The f32 shapes rarely
+    // spill at their table sizes and measured 0.8 % slower with it (profiles/r03/search_experiments/).
+    constexpr bool kSpillPrefetch = kSpace != 0;
+    uint32_t pre_u = kEmpty, pre_w = 0u;
     while (ps.cur < ps.size) {
       const uint32_t u = pool_pop(ps, L);
       ++n_expand;
@@ -321,7 +327,7 @@ __global__ void __launch_bounds__(256)
         }
       }
       if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs);
-      const bool fresh = visit(vs, v, act);
+      const bool fresh = visit(vs, v, act, kSpillPrefetch && u == pre_u, pre_w);
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
       // issue the prefetch only after v is consumed: a use of v behind a younger load would
@@ -339,6 +345,14 @@ __global__ void __launch_bounds__(256)
       if (fresh) L.cid[slot] = v;
       wave_sync();
       space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd);
+      if constexpr (kSpillPrefetch) {
+        pre_u = kEmpty;
+        if (vs.spilled && pred != kEmpty) {
+          __builtin_amdgcn_s_waitcnt(0);  // this expansion's second-level atomics have landed in L2
+          pre_w = spill_prefetch(vs, pred_v, lane < static_cast<int>(p.R));
+          pre_u = pred;
+        }
+      }
       stamp(3);
       n_dist += nf;
       const bool has = lane < nf;
