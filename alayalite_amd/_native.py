@@ -14,22 +14,18 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 def _runtime_order():
     """PyTorch-ROCm bundles its own HIP + HSA runtime (torch/lib) beside /opt/rocm's, which this
-    engine links.  Both live in one process only in one order: torch's runtime loaded and
-    initialised first, then the engine's.  Loading the engine first left the engine with no device
-    ("no HIP device available") once torch initialised afterwards (a GPU test run, r03), and
-    initialising the engine first leaves torch without devices.  So when torch is importable it is
-    loaded and initialised here, before the extension (ALAYA_SKIP_TORCH_INIT=1 skips it for
-    processes that never use torch, e.g. the sanitizer driver)."""
+    engine links.  torch's libraries are loaded first (a plain ``import torch``), so the engine's
+    HIP soname resolves to the runtime torch uses.  Nothing is initialised here: importing the
+    package starts no GPU runtime (a later fork or exec stays safe), and the first device call --
+    the engine's or torch's, in either order -- initialises the one runtime
+    (tools/runtime_order_probe.py, profiles/r04/runtime_order.log).  ALAYA_SKIP_TORCH_INIT=1 skips
+    the torch import for processes that never use torch (e.g. the sanitizer driver)."""
     if os.environ.get("ALAYA_SKIP_TORCH_INIT") == "1":
         return
     try:
-        import torch
+        import torch  # noqa: F401  (loads the libraries; no device call)
     except ImportError:  # the engine itself does not need torch
         return
-    try:
-        torch.cuda.is_available()
-    except Exception:  # pragma: no cover
-        pass
 
 
 def _load():

@@ -119,8 +119,9 @@ struct alaya_index {
   bool norms_ready = false;
   float max_norm = 0.f;
   // scratch
-  DevBuf work, overflow, dirty, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
+  DevBuf work, overflow, dirty, stab, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
   size_t overflow_clean = 0;  // leading bytes of `overflow` known to be zero (kernels leave it clean)
+  size_t stab_clean = 0;      // the same for the spill tables
   uint32_t hash_log2_override = 0;
   int visited_mode_override = 0;  // 0 auto, 1 compact 16-bit slots, 2 wide 32-bit slots,
                                   // 3 compact with probes capped at 2 (exercises the probe spill)
@@ -140,7 +141,8 @@ struct alaya_index {
   bool scratch_used = false;
   uint64_t device_bytes() const {
     return base.bytes + valid.bytes + l0.bytes + levels.bytes + upper_off.bytes +
-           upper_edges.bytes + eps.bytes + overflow.bytes + codes.bytes + sq_min.bytes + sq_max.bytes;
+           upper_edges.bytes + eps.bytes + overflow.bytes + dirty.bytes + stab.bytes + codes.bytes + sq_min.bytes +
+           sq_max.bytes;
   }
 };
 
@@ -159,9 +161,32 @@ void scratch_release(alaya_index *ix, hipStream_t s) {
   ix->scratch_stream = s;
   ix->scratch_used = true;
 }
+// The visited spill areas (bitsets, spill tables) are zeroed once and then kept clean by every
+// query that finishes.  A launch or sync that reports an error may have left a query half done, so
+// the next launch zeroes them again.
+void scratch_suspect(alaya_index *ix) {
+  ix->overflow_clean = 0;
+  ix->stab_clean = 0;
+}
 // Wait (host side) until no launch can still read or write the index's device buffers.
 void scratch_drain(alaya_index *ix) {
-  if (ix->scratch_used) hip_check(hipEventSynchronize(ix->scratch_ev), "hipEventSynchronize");
+  if (!ix->scratch_used) return;
+  const hipError_t e = hipEventSynchronize(ix->scratch_ev);
+  if (e != hipSuccess) scratch_suspect(ix);
+  hip_check(e, "hipEventSynchronize");
+}
+// guarded() for the entry points that launch searches on the index's scratch: a device error marks
+// the spill areas for re-zeroing.
+template <typename F>
+int guarded_scratch(alaya_index *ix, F &&f) {
+  return guarded([&] {
+    try {
+      f();
+    } catch (const DeviceError &) {
+      if (ix) scratch_suspect(ix);
+      throw;
+    }
+  });
 }
 
 SearchParams base_params(alaya_index *ix) {
@@ -179,8 +204,32 @@ SearchParams base_params(alaya_index *ix) {
 constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr uint32_t kDirtyCap = 16384;  // per-slot dirty-word list (64 KB): words a spilled query set
 
+// Spill table size (log2 entries per slot) for an AVX-512-order SQ8 search, 0 = the bitset is the
+// second level.
+// ~32 ef entries (config 5, ef 340: 2^14 = 32 KB per slot for ~2.7k visited ids, load 0.16, so a
+// full bucket of 8 -- the bitset fallback -- is rare); at least 2^(L - 12) so an entry (1 + the
+// hash's low L - (s - 3) bits) fits 16 bits; at most 2^16 (128 KB per slot; ids wider than 28 bits
+// keep the bitset).  ALAYA_SPILL_TABLE=0 keeps the bitset, a value 6..16 forces the size (tests: tiny
+// tables fill their buckets and exercise the bitset fallback).
+uint32_t spill_table_log2(int sq8_order, uint32_t L, uint32_t ef) {
+  // f32 kernels: their tables rarely spill, they keep the bitset; so do the AVX2-order SQ8 kernels
+  // (hosts without AVX-512), whose SGPR budget the table's state would overrun (65-116 restores per
+  // expansion)
+  if (sq8_order != 2) return 0;
+  uint32_t s = std::max<uint32_t>({6u, ceil_log2(32ull * ef), L > 12 ? L - 12 : 0u});
+  if (const char *e = std::getenv("ALAYA_SPILL_TABLE")) {
+    const uint32_t v = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+    if (v == 0) return 0;
+    if (v >= 6 && v <= 16) s = v;
+  }
+  s = std::min<uint32_t>(s, L + 3);  // buckets <= 2^L: the bucket index is the hash's top bits
+  if (s > 16 || s < 6 || L - (s - 3) > 15) return 0;
+  return s;
+}
+
 // The visited set's second level for `slots` persistent searchers over ix->n rows: one clean N-bit
-// bitset per slot (zeroed once when allocated; every query leaves it clean) and a dirty-word list.
+// bitset per slot (zeroed once when allocated; every query leaves it clean) and a dirty-word list,
+// plus (SQ8 searches, spill_table_log2) one clean spill table per slot.
 void prepare_spill(alaya_index *ix, SearchParams &p, uint64_t slots, hipStream_t stream) {
   const uint64_t words = (ix->n + 31) / 32;
   const size_t bytes = static_cast<size_t>(std::max<uint64_t>(slots, 1)) * words * 4;
@@ -198,6 +247,25 @@ void prepare_spill(alaya_index *ix, SearchParams &p, uint64_t slots, hipStream_t
   p.overflow_bits = ix->overflow.as<uint32_t>();
   p.dirty_words = ix->dirty.as<uint32_t>();
   p.dirty_cap = cap;
+  p.spill_table = nullptr;
+  p.stab_log2 = p.stab_rbits = 0;
+  p.spill_flags = 0;
+  if (const char *e = std::getenv("ALAYA_SPILL_FLAGS")) p.spill_flags = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+  if (const uint32_t st = spill_table_log2(p.sq8_order, p.vis_lbits, p.ef)) {
+    const size_t tbytes = static_cast<size_t>(std::max<uint64_t>(slots, 1)) * (2ull << st);
+    if (tbytes > ix->stab.bytes) {
+      ix->stab.reserve(tbytes);
+      ix->stab_clean = 0;
+    }
+    if (ix->stab_clean < ix->stab.bytes) {
+      hip_check(hipMemsetAsync(ix->stab.ptr, 0, ix->stab.bytes, stream), "hipMemsetAsync");
+      ix->stab_clean = ix->stab.bytes;
+    }
+    const uint32_t rbits = p.vis_lbits - (st - 3);
+    p.spill_table = ix->stab.as<uint16_t>();
+    p.stab_log2 = st;
+    p.stab_rbits = rbits;
+  }
 }
 
 // Waves per search workgroup: SQ8 searchers share the quantizer's per-dimension scale and min
@@ -260,8 +328,13 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   }
   const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0);
   const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
+  // the register-bound residency, probed with a 4 KB table -- or with the smallest table when a
+  // spill table is the second level (a spill then costs a flush and prefetched bucket reads, not a
+  // round trip per visit, so residency wins over first-level size)
+  const bool stab = spill_table_log2(p.sq8_order, lbits, ef) != 0;
   int vgpr_blocks = 0;
-  hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + 4096), &vgpr_blocks), "occupancy");
+  hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + (stab ? 1024 : 4096)), &vgpr_blocks),
+            "occupancy");
   const uint64_t vgpr_waves = static_cast<uint64_t>(std::max(1, vgpr_blocks)) * W;
   const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
   const uint64_t max_waves = std::max<uint64_t>(W, max_search_waves_per_cu());
@@ -903,7 +976,7 @@ int alaya_index_enable_updates(alaya_index *ix, const alaya_graph *g, const floa
 
 int alaya_index_insert(alaya_index *ix, const float *search_query, const float *row, uint32_t ef,
                        uint64_t *new_id) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || !search_query || !row || !new_id) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1058,7 +1131,7 @@ extern "C" {
 int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_construction, uint64_t seed,
                             uint32_t batch_div, uint32_t max_batch, uint32_t refine, alaya_graph **out,
                             uint64_t *stats) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix) throw ArgError("invalid arguments");
     if (R < 2 || R > 64 || R % 2) throw ArgError("max_nbrs must be even and in 2..64 for the device build");
     std::lock_guard<std::mutex> lk(ix->mu);
@@ -1243,7 +1316,7 @@ int alaya_index_build_graph(alaya_index *ix, uint32_t R, uint32_t ef_constructio
 int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uint64_t nq,
                                     uint32_t k, uint32_t ef, uint32_t *d_ids, float *d_dists,
                                     uint32_t *d_counters, void *stream) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!d_queries || !d_ids))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1255,7 +1328,7 @@ int alaya_index_batch_search_device(alaya_index *ix, const float *d_queries, uin
 int alaya_index_shard_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
                                     uint32_t ef, uint32_t *d_ids, float *d_dists, uint32_t *d_counters,
                                     void *stream) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!d_queries || !d_ids || !d_dists))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1266,7 +1339,7 @@ int alaya_index_shard_search_device(alaya_index *ix, const float *d_queries, uin
 
 int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
                              uint32_t ef, uint32_t *ids, float *dists, uint32_t *counters) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1290,7 +1363,7 @@ int alaya_index_batch_search(alaya_index *ix, const float *queries, uint64_t nq,
 
 int alaya_index_profile_search(alaya_index *ix, const float *queries, uint64_t nq, uint32_t k,
                                uint32_t ef, int space, uint32_t *ids, uint32_t *counters, uint64_t *stamps) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!queries || !ids || !stamps))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1457,7 +1530,7 @@ static void sq8_search_dev(alaya_index *ix, const float *d_q, const float *d_rq,
 int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const float *rerank_queries,
                                  uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *ids,
                                  float *dists, uint32_t *counters) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!queries || !ids))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1487,7 +1560,7 @@ int alaya_index_batch_search_sq8(alaya_index *ix, const float *queries, const fl
 int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
                                         uint64_t nq, uint32_t k, uint32_t ef, int rerank, uint32_t *d_ids,
                                         float *d_dists, uint32_t *d_counters, void *stream) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!d_queries || !d_ids))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);
@@ -1499,7 +1572,7 @@ int alaya_index_batch_search_sq8_device(alaya_index *ix, const float *d_queries,
 int alaya_index_shard_search_sq8_device(alaya_index *ix, const float *d_queries, const float *d_rerank_queries,
                                         uint64_t nq, uint32_t k, uint32_t ef, int holds_row0, uint32_t *d_ids,
                                         float *d_dists, uint32_t *d_counters, void *stream) {
-  return guarded([&] {
+  return guarded_scratch(ix, [&] {
     if (!ix || (nq && (!d_queries || !d_ids || !d_dists))) throw ArgError("invalid arguments");
     std::lock_guard<std::mutex> lk(ix->mu);
     set_device(ix);

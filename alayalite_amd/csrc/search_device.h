@@ -579,13 +579,17 @@ struct Visited {
   uint32_t ndirty;       // wave-uniform number of words appended (may exceed dirty_cap)
   uint64_t n_words;      // bitset words (ceil(n / 32))
   uint32_t rbits;        // compact: remainder bits; kVisWide: 32-bit slots
-  uint32_t lmask;        // compact: 2^L - 1
+  uint32_t lmask;        // 2^L - 1 (compact slots and the spill table hash with it)
   uint32_t lshift;       // compact, L < log2h: home = h << lshift
   uint32_t max_disp;     // compact: largest encodable probe distance
+  // spill table (SQ8 kernels, SearchParams::spill_table): nullptr = the bitset is the second level
+  uint16_t *stab;
+  uint32_t stab_bmask;   // buckets - 1
+  uint32_t stab_rbits;
 };
 
 __device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t *tab, uint32_t *bits,
-                                                uint32_t *dirty) {
+                                                uint32_t *dirty, uint16_t *stab = nullptr) {
   Visited vs;
   vs.tab = tab;
   vs.log2h = p.hash_log2;
@@ -596,14 +600,17 @@ __device__ __forceinline__ Visited make_visited(const SearchParams &p, uint32_t 
   vs.dirty_cap = p.dirty_cap;
   vs.ndirty = 0u;
   vs.n_words = (p.n + 31) / 32;
+  vs.stab = stab;
+  vs.stab_bmask = stab ? (1u << (p.stab_log2 - 3)) - 1u : 0u;
+  vs.stab_rbits = p.stab_rbits;
   vs.rbits = p.vis_rbits;
   const uint32_t hsize = 1u << p.hash_log2;
+  vs.lmask = p.vis_lbits >= 32 ? 0xffffffffu : (1u << p.vis_lbits) - 1u;  // compact slots, spill table
   if (p.vis_rbits == kVisWide) {
     vs.limit = hsize / 2;
-    vs.lmask = vs.lshift = vs.max_disp = 0u;
+    vs.lshift = vs.max_disp = 0u;
   } else {
     vs.limit = hsize - hsize / 4 - hsize / 16;  // load factor 0.69
-    vs.lmask = p.vis_lbits >= 32 ? 0xffffffffu : (1u << p.vis_lbits) - 1u;
     vs.lshift = p.vis_lbits < p.hash_log2 ? p.hash_log2 - p.vis_lbits : 0u;
     vs.max_disp = p.vis_max_disp;
   }
@@ -677,16 +684,168 @@ __device__ __forceinline__ int table_insert(const Visited &vs, uint32_t v) {
   return 2;
 }
 
-// The global bitset becomes the second level; it is already clean (no zeroing here).
-__device__ __forceinline__ void spill_begin(Visited &vs) { vs.spilled = true; }
+// The lane that set a bitset word's first bit records the word on the slot's dirty list (visit_end
+// clears exactly those words).  Wave-uniform.
+__device__ __forceinline__ void dirty_append(Visited &vs, bool first, uint32_t word) {
+  const uint64_t fm = ballot(first);
+  if (fm) {
+    const uint32_t pos = vs.ndirty + __popcll(fm & ((1ull << lane_id()) - 1ull));
+    if (first && pos < vs.dirty_cap) vs.dirty[pos] = word;
+    vs.ndirty += __popcll(fm);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Spill table: the second level of the SQ8 kernels (config 5: 10M ids fit only a few hundred LDS
+// slots at full residency, so ~90 % of a query's expansions run spilled).  Per slot, 2^s 16-bit
+// entries in buckets of 8 (16 B), zero = empty, clean between queries.  h = (v * C) mod 2^L is a
+// bijection (L = vis_lbits >= log2 n, C odd); the home bucket is h's top s - 3 bits and an entry
+// stores 1 + h's low rbits bits, so (bucket, entry) identifies v.  An id
+// goes into its home bucket's first free entry, or -- when the bucket is full -- into the bitset
+// (third level).  Buckets fill in entry order and nothing is removed during a query, so a bucket
+// that is not full has never been full: v is visited iff its home bucket holds it, or the bucket is
+// full and the bitset holds it.
+// At 32 KB per slot (config 5: 2^14 entries for ~2.7k visited ids, load 0.16) every table of a
+// launch fits the Infinity Cache, where the N-bit bitsets took 1.25 MB per slot (3.8 GB) and every
+// visit was a scattered line in HBM.  The wave is the slot's only writer: entries are plain 16-bit
+// stores, no atomics.  Reads are agent-scope (L2, never a stale vector-L1 line).
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ void stab_key(const Visited &vs, uint32_t v, uint32_t &home, uint32_t &code) {
+  const uint32_t h = (v * 0x9E3779B1u) & vs.lmask;
+  home = h >> vs.stab_rbits;  // the host keeps buckets <= 2^L: rbits >= 0
+  code = 1u + (h & ((1u << vs.stab_rbits) - 1u));
+}
+
+__device__ __forceinline__ void stab_load(const Visited &vs, uint32_t bucket, uint64_t &lo, uint64_t &hi) {
+  uint64_t *b = reinterpret_cast<uint64_t *>(vs.stab + static_cast<size_t>(bucket) * kStabBucket);
+  lo = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  hi = __hip_atomic_load(b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Stores are agent-scope too: a plain (CU-scope) store may be acknowledged before it reaches L2, where
+// the wave's next agent-scope read of the bucket looks (measured: duplicate visits with plain stores).
+__device__ __forceinline__ void stab_store(const Visited &vs, uint32_t entry, uint32_t code) {
+  __hip_atomic_store(vs.stab + entry, static_cast<uint16_t>(code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// found: the bucket holds `code`; occ: entries in use (= the first free position)
+__device__ __forceinline__ void stab_scan(uint64_t lo, uint64_t hi, uint32_t code, bool &found, uint32_t &occ) {
+  found = false;
+  occ = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t a = static_cast<uint32_t>(lo >> (16 * j)) & 0xffffu;
+    const uint32_t b = static_cast<uint32_t>(hi >> (16 * j)) & 0xffffu;
+    found |= (a == code) | (b == code);
+    occ += (a != 0u ? 1u : 0u) + (b != 0u ? 1u : 0u);
+  }
+}
+
+// Visit on the spill table.  Lanes with `act` hold distinct ids.  pre_ok (wave-uniform): (lo, hi)
+// hold each lane's home bucket as it is now (stab_prefetch after the previous expansion's stores had
+// landed; nothing is stored in between); otherwise the buckets are loaded here.
+__device__ __forceinline__ bool stab_visit(Visited &vs, uint32_t v, bool act, bool pre_ok, uint64_t lo, uint64_t hi) {
+  const int lane = lane_id();
+  uint32_t home = 0, code = 0;
+  stab_key(vs, v, home, code);
+  if (!pre_ok) {
+    __builtin_amdgcn_s_waitcnt(0);  // every earlier store of this wave has landed in L2
+    if (act) stab_load(vs, home, lo, hi);
+  }
+  bool found;
+  uint32_t occ;
+  stab_scan(lo, hi, code, found, occ);
+  // home bucket with room and v not in it: v is nowhere (not in the bitset either) -> fresh; it
+  // takes position occ + (fresh lanes below it with the same home bucket)
+  const bool fast = act && !found && occ < kStabBucket;
+  const uint64_t fm = ballot(fast);
+  uint32_t rank = 0;
+  for (uint64_t r = fm; r; r &= r - 1) {
+    const int j = __ffsll(static_cast<unsigned long long>(r)) - 1;
+    rank += (j < lane && read_lane(home, j) == home) ? 1u : 0u;
+  }
+  const bool placed = fast && occ + rank < kStabBucket;
+  if (placed) stab_store(vs, home * kStabBucket + occ + rank, code);
+  // rare: the home bucket is full (v may be in the bitset) or filled up within this visit (v is
+  // fresh): the bitset, one returning atomic per such lane
+  const bool third = act && !found && !placed;
+  if (ballot(third)) {
+    const uint32_t bit = 1u << (v & 31);
+    uint32_t old = bit;
+    if (third) old = atomicOr(&vs.bits[v >> 5], bit);
+    dirty_append(vs, third && old == 0u, v >> 5);
+    return placed || (third && (old & bit) == 0u);
+  }
+  return placed;
+}
+
+// After an expansion's distances (its visits are complete: the wave waited for its row loads, which
+// were issued after them, and for its stores), read the spill-table home buckets of the predicted
+// next expansion's neighbours (`row_v`, lane-aligned as the next visit will see them).  Used only if
+// the prediction holds.
+__device__ __forceinline__ void stab_prefetch(const Visited &vs, uint32_t row_v, bool lane_in_row, uint64_t &lo,
+                                              uint64_t &hi) {
+  lo = hi = 0ull;
+  if (lane_in_row && row_v != kEmpty) {
+    uint32_t home, code;
+    stab_key(vs, row_v, home, code);
+    stab_load(vs, home, lo, hi);
+  }
+}
+
+// Spill with the table as the second level: every id the LDS table holds goes into the spill table
+// (compact slots decode back to ids: (slot, probe distance, remainder) gives the hash h, and h times
+// the inverse of the multiplicative constant mod 2^L gives v), so a spilled visit never consults
+// the LDS table again.  Wave-uniform; table sizes are multiples of 64 slots.
+__device__ void stab_flush(Visited &vs) {
+  vs.spilled = true;
+  const int lane = lane_id();
+  const uint32_t hsize = 1u << vs.log2h;
+  const uint32_t mask = hsize - 1u;
+  wave_sync();
+  for (uint32_t b = 0; b < hsize; b += 64) {
+    const uint32_t slot = b + static_cast<uint32_t>(lane);
+    uint32_t v = kEmpty;
+    if (vs.rbits == kVisWide) {
+      v = vs.tab[slot];
+    } else {
+      const uint32_t e = reinterpret_cast<const uint16_t *>(vs.tab)[slot];
+      if (e != 0u) {
+        const uint32_t x = e - 1u;
+        const uint32_t i = x >> vs.rbits;
+        const uint32_t rem = x & ((1u << vs.rbits) - 1u);
+        const uint32_t home = (slot - i) & mask;
+        const uint32_t h = vs.rbits ? ((home << vs.rbits) | rem) : (home >> vs.lshift);
+        v = (h * 0x0E8B2F51u) & vs.lmask;  // 0x9E3779B1 * 0x0E8B2F51 == 1 (mod 2^32)
+      }
+    }
+    const bool has = v != kEmpty;
+    if (ballot(has)) stab_visit(vs, v, has, false, 0ull, 0ull);
+  }
+}
+
+// The second level takes over (the bitset is already clean; the spill table gets the LDS entries).
+template <bool kTab = false>
+__device__ __forceinline__ void spill_begin(Visited &vs) {
+  if (kTab && vs.stab != nullptr) {
+    stab_flush(vs);
+  } else {
+    vs.spilled = true;
+  }
+}
 
 // All lanes with `act` insert their v; duplicates among lanes must have been removed.
-// pre_ok (wave-uniform): pre_w holds, per lane, the current value of the second-level word of this
-// lane's v (spill_prefetch below, issued for exactly this adjacency row after the previous expansion's
-// visits had completed; the wave is the slot's only writer and nothing is visited in between).  A set
-// bit then means visited without a round trip, and a clear one means fresh unless the (read-only)
-// first level holds v: its bit is set by an atomic whose result nobody waits for.
-__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, bool pre_ok, uint32_t pre_w) {
+// pre_ok (wave-uniform): (pre_lo, pre_hi) hold the lane's second-level state for its v, read one
+// expansion ahead (spill_prefetch below, issued for exactly this adjacency row after the previous
+// expansion's visits had completed; the wave is the slot's only writer and nothing is visited in
+// between).  Spill table: the v's home bucket (stab_visit).  Bitset: pre_lo's low word is v's bitset
+// word -- a set bit means visited without a round trip, and a clear one means fresh unless the
+// (read-only) first level holds v: its bit is set by an atomic whose result nobody waits for.
+template <bool kTab = false>
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, bool pre_ok, uint64_t pre_lo,
+                                      uint64_t pre_hi) {
+  if (kTab && vs.spilled && vs.stab != nullptr) return stab_visit(vs, v, act, pre_ok, pre_lo, pre_hi);
+  const uint32_t pre_w = static_cast<uint32_t>(pre_lo);
   bool fresh = false;
   bool global = false;
   if (!vs.spilled) {
@@ -695,6 +854,11 @@ __device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, bool pr
     fresh = r == 1;
     vs.count += __popcll(ballot(fresh));
     if (ballot(r == 2)) {  // a compact probe ran out of encodable distance: spill now
+      if (kTab && vs.stab != nullptr) {
+        stab_flush(vs);  // this visit's LDS inserts included; the lanes that failed go to the table
+        const bool f2 = stab_visit(vs, v, r == 2, false, 0ull, 0ull);
+        return fresh || f2;
+      }
       spill_begin(vs);
       global = r == 2;
     }
@@ -714,42 +878,53 @@ __device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act, bool pr
     }
     // the lane that set a word's first bit records the word (at most one lane per word: the
     // atomics of one wave to one word are serialised, the later ones see the earlier bits)
-    const bool first = global && old == 0u;
-    const uint64_t fm = ballot(first);
-    if (fm) {
-      const uint32_t pos = vs.ndirty + __popcll(fm & ((1ull << lane_id()) - 1ull));
-      if (first && pos < vs.dirty_cap) vs.dirty[pos] = v >> 5;
-      vs.ndirty += __popcll(fm);
-    }
+    dirty_append(vs, global && old == 0u, v >> 5);
   }
   return fresh;
 }
 
-__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) { return visit(vs, v, act, false, 0u); }
-
-// After an expansion's distances (its visits are complete: the wave waited for its row loads, which
-// were issued after them), read the second-level words of the predicted next expansion's adjacency
-// row (`row`, lane-aligned as the next visit will see it).  The load is agent-scope so it reads L2,
-// where the wave's own atomics landed, not a stale vector-L1 copy.  Used only if the prediction holds.
-__device__ __forceinline__ uint32_t spill_prefetch(const Visited &vs, uint32_t row_v, bool lane_in_row) {
-  uint32_t w = 0u;
-  if (lane_in_row && row_v != kEmpty)
-    w = __hip_atomic_load(&vs.bits[row_v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return w;
+template <bool kTab = false>
+__device__ __forceinline__ bool visit(Visited &vs, uint32_t v, bool act) {
+  return visit<kTab>(vs, v, act, false, 0ull, 0ull);
 }
 
-// End of a query: leave the slot's bitset clean for the next one (the words on the dirty list, or
-// the whole bitset when the list overflowed).  Wave-uniform.
+// After an expansion's distances (its visits are complete: the wave waited for its row loads, which
+// were issued after them), read the second-level state of the predicted next expansion's adjacency
+// row (`row`, lane-aligned as the next visit will see it): the spill table's home buckets, or the
+// bitset words.  The loads are agent-scope so they read L2, where the wave's own stores and atomics
+// landed, not a stale vector-L1 copy.  Used only if the prediction holds.
+__device__ __forceinline__ void spill_prefetch(const Visited &vs, uint32_t row_v, bool lane_in_row, uint64_t &lo,
+                                               uint64_t &hi) {
+  if (vs.stab != nullptr) {
+    stab_prefetch(vs, row_v, lane_in_row, lo, hi);
+    return;
+  }
+  lo = hi = 0ull;
+  if (lane_in_row && row_v != kEmpty)
+    lo = __hip_atomic_load(&vs.bits[row_v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// End of a query: leave the slot's second level clean for the next one -- the spill table whole, and
+// the bitset's words on the dirty list (or the whole bitset when the list overflowed).  Wave-uniform.
 __device__ __forceinline__ void visit_end(Visited &vs) {
   if (!vs.spilled) return;
   const int lane = lane_id();
   __threadfence_block();  // this wave's dirty-list stores are visible to its own loads below
+  if (vs.stab != nullptr) {  // agent-scope stores: the next query's agent-scope reads see the zeros
+    uint64_t *t = reinterpret_cast<uint64_t *>(vs.stab);
+    const uint32_t n8 = 2u * (vs.stab_bmask + 1u);  // two 8-byte halves per bucket
+    for (uint32_t i = lane; i < n8; i += 64) __hip_atomic_store(t + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // agent-scope stores: the next query's atomics (performed in L2) must find them there
   if (vs.ndirty <= vs.dirty_cap) {
-    for (uint32_t i = lane; i < vs.ndirty; i += 64) vs.bits[vs.dirty[i]] = 0u;
+    for (uint32_t i = lane; i < vs.ndirty; i += 64)
+      __hip_atomic_store(&vs.bits[vs.dirty[i]], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    for (uint64_t w = lane; w < vs.n_words; w += 64) vs.bits[w] = 0u;
+    for (uint64_t w = lane; w < vs.n_words; w += 64)
+      __hip_atomic_store(&vs.bits[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __threadfence_block();  // the clearing stores land before the slot's next query sets bits
+  __builtin_amdgcn_s_waitcnt(0);  // (and before its agent-scope spill-table reads)
   vs.spilled = false;
 }
 

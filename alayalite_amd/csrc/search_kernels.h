@@ -55,6 +55,14 @@ struct SearchParams {
   uint32_t vis_max_disp;  // compact: largest probe distance an entry may sit at (<= 0xffff >> rbits - 1)
   uint32_t vis_limit;     // LDS table entries before a query spills to the second level (0 = the
                           // layout's default: half the slots wide, 11/16 compact); <= slots - 64
+  // Spill table (stab_log2 != 0): the second level is a per-slot hash table of 2^stab_log2 16-bit
+  // entries in buckets of 8 (16 B), all zero between queries, instead of the N-bit bitset; the bitset
+  // stays as a third level for the (rare) ids whose home bucket is full.  An entry is 1 + the low
+  // stab_rbits bits of the vis_lbits-bit bijective hash, whose top bits are the bucket.
+  uint16_t *spill_table;  // slots x 2^stab_log2 entries
+  uint32_t stab_log2;
+  uint32_t stab_rbits;    // <= 15
+  uint32_t spill_flags;   // diagnostics (ALAYA_SPILL_FLAGS): bit 0 = no second-level prefetch
   uint64_t *stamps;       // nullable: diagnostic per-phase cycle counts, nq x 8
   // SQ8 search space (SQ8Space, space/sq8_space.hpp): traversal distances on uint8 codes
   int sq8_order;          // 0 = f32 RawSpace search; 2 = AVX-512 SQ8 order; 1 = AVX2 SQ8 order
@@ -84,6 +92,7 @@ struct RerankParams {
 };
 
 constexpr uint32_t kVisWide = 0xffffffffu;
+constexpr uint32_t kStabBucket = 8;  // spill-table entries per bucket (16 B: one prefetch per lane)
 // bytes of the LDS visited table / of one wave's LDS region / of a workgroup's shared region
 // (SQ8: the quantizer's per-dimension scale and min); a workgroup of W waves takes
 // shared + W * wave bytes

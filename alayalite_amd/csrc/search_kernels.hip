@@ -26,14 +26,23 @@
 // budget: 512 / waves VGPRs).  0 = no constraint.  Diagnostics builds override with
 // -DALAYA_MIN_WAVES_SQ8=... / -DALAYA_MIN_WAVES_NARROW=....
 #ifndef ALAYA_MIN_WAVES_SQ8
-#define ALAYA_MIN_WAVES_SQ8 0
+// The AVX-512-order SQ8 kernels (config 5 on an AVX-512 host) are held to 4 waves per SIMD (128
+// VGPRs): with the spill table the 768-d IP kernel needs 129 and would drop to 3; at 128 the
+// allocator spills one 8-byte value that is live across the whole query loop (a store at kernel
+// entry, a load after the loop), nothing per expansion.  The AVX2-order kernels would spill inside
+// the expansion loop (32-136 B of scratch) and keep their natural budget.
+#define ALAYA_MIN_WAVES_SQ8 -1
 #endif
 #ifndef ALAYA_MIN_WAVES_NARROW
 #define ALAYA_MIN_WAVES_NARROW 0
 #endif
 template <int kChunks, int kSpace>
 constexpr int search_min_waves() {
-  return kSpace != 0 ? ALAYA_MIN_WAVES_SQ8 : (kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : 0);
+  if constexpr (kSpace != 0) {
+    if (ALAYA_MIN_WAVES_SQ8 >= 0) return ALAYA_MIN_WAVES_SQ8;
+    return kSpace == 2 && kChunks > 0 ? 4 : 0;
+  }
+  return kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : 0;
 }
 
 namespace alaya_amd {
@@ -88,7 +97,7 @@ __device__ __forceinline__ void fill_shared(const SearchParams &p, const Lds &L)
 // quantizer), visited table and pool cleared, then Graph::initialize_search (graph.hpp:148-158).
 template <bool kIP, int kChunks, int kSpace>
 __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L, uint32_t qi, uint32_t *slot_bits,
-                                            uint32_t *slot_dirty, Visited &vs, PoolState &ps,
+                                            uint32_t *slot_dirty, uint16_t *slot_stab, Visited &vs, PoolState &ps,
                                             uint32_t &n_dist_up, uint32_t &n_hops_up) {
   const int lane = lane_id();
   const uint32_t hsize = 1u << p.hash_log2;
@@ -127,8 +136,9 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
     L.pi[e] = 0u;
   }
   wave_sync();
-  vs = make_visited(p, L.hash, slot_bits, slot_dirty);
+  vs = make_visited(p, L.hash, slot_bits, slot_dirty, slot_stab);
   ps = PoolState{0u, 0u, p.ef};
+  constexpr bool kTab = kSpace == 2;  // the AVX-512-order SQ8 kernels may run on the spill table
 
   // ---- Graph::initialize_search (graph.hpp:148-158) ---------------------------------------
   if (p.levels != nullptr) {
@@ -189,7 +199,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
     }
     ps.size = 1;
     ps.cur = 0;
-    visit(vs, u, lane == 0);
+    visit<kTab>(vs, u, lane == 0);
     wave_sync();
   } else {
     // NSG-style entry points: insert each ep, then mark it visited (graph.hpp:153-156)
@@ -209,8 +219,8 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
       // duplicates among eps are all inserted (no visited check in the reference loop)
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t vj = read_lane(v, j);
-        if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs);
-        visit(vs, vj, lane == 0);
+        if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin<kTab>(vs);
+        visit<kTab>(vs, vj, lane == 0);
       }
       wave_sync();
     }
@@ -264,6 +274,8 @@ __global__ void __launch_bounds__(256)
   const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
   uint32_t *slot_bits = p.overflow_bits + slot * bit_words;
   uint32_t *slot_dirty = p.dirty_words + slot * p.dirty_cap;
+  // spill tables only in the SQ8 kernels (a compile-time null elsewhere: the f32 kernels carry none of it)
+  uint16_t *slot_stab = (kSpace == 2 && p.spill_table) ? p.spill_table + (slot << p.stab_log2) : nullptr;
 
   for (;;) {
     uint32_t qi = 0;
@@ -284,7 +296,7 @@ __global__ void __launch_bounds__(256)
     Visited vs;
     PoolState ps;
     uint32_t n_dist = 0, n_expand = 0, n_dist_up = 0, n_hops_up = 0;
-    query_begin<kIP, kChunks, kSpace>(p, L, qi, slot_bits, slot_dirty, vs, ps, n_dist_up, n_hops_up);
+    query_begin<kIP, kChunks, kSpace>(p, L, qi, slot_bits, slot_dirty, slot_stab, vs, ps, n_dist_up, n_hops_up);
 
     // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
     stamp(0);
@@ -292,12 +304,14 @@ __global__ void __launch_bounds__(256)
     // expansion unless the merge puts a closer candidate in front of it.  Its 128 B row is loaded
     // into registers while this expansion runs and used only if the next pop returns that id.
     uint32_t pred = kEmpty, pred_v = kEmpty;
-    // Second-level visited words of the predicted next expansion (spilled queries, spill_prefetch):
-    // the SQ8 kernels only, where config 5's 10k-query batch spills almost every query (its 10M ids
-    // fit only a few hundred LDS slots at full residency): 10.43 -> 9.76 ms.  The f32 shapes rarely
-    // spill at their table sizes and measured 0.8 % slower with it (profiles/r03/search_experiments/).
+    // Second-level state of the predicted next expansion's neighbours (spilled queries,
+    // spill_prefetch: spill-table buckets or bitset words): the SQ8 kernels only, where config 5's
+    // 10k-query batch spills almost every query (its 10M ids fit only a few hundred LDS slots at full
+    // residency): 10.43 -> 9.76 ms with the bitset.  The f32 shapes rarely spill at their table
+    // sizes and measured 0.8 % slower with it (profiles/r03/search_experiments/).
     constexpr bool kSpillPrefetch = kSpace != 0;
-    uint32_t pre_u = kEmpty, pre_w = 0u;
+    uint32_t pre_u = kEmpty;
+    uint64_t pre_lo = 0ull, pre_hi = 0ull;
     while (ps.cur < ps.size) {
       const uint32_t u = pool_pop(ps, L);
       ++n_expand;
@@ -326,8 +340,14 @@ __global__ void __launch_bounds__(256)
           if (j < lane && vj == v) act = false;
         }
       }
-      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin(vs);
-      const bool fresh = visit(vs, v, act, kSpillPrefetch && u == pre_u, pre_w);
+      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin<kSpace == 2>(vs);
+      const bool fresh = visit<kSpace == 2>(vs, v, act, kSpillPrefetch && u == pre_u, pre_lo, pre_hi);
+      // consumed: the prefetched state describes the table only up to this visit's stores, so it
+      // is never reused (an expansion without fresh neighbours skips the prefetch below, and the
+      // next pop must not take this one for its own); zeroed so it is not live across the
+      // distance phase either
+      pre_u = kEmpty;
+      pre_lo = pre_hi = 0ull;
       const uint64_t fm = ballot(fresh);
       const int nf = __popcll(fm);
       // issue the prefetch only after v is consumed: a use of v behind a younger load would
@@ -346,10 +366,9 @@ __global__ void __launch_bounds__(256)
       wave_sync();
       space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd);
       if constexpr (kSpillPrefetch) {
-        pre_u = kEmpty;
-        if (vs.spilled && pred != kEmpty) {
-          __builtin_amdgcn_s_waitcnt(0);  // this expansion's second-level atomics have landed in L2
-          pre_w = spill_prefetch(vs, pred_v, lane < static_cast<int>(p.R));
+        if (vs.spilled && pred != kEmpty && !(p.spill_flags & 1u)) {
+          __builtin_amdgcn_s_waitcnt(0);  // this expansion's second-level stores / atomics have landed in L2
+          spill_prefetch(vs, pred_v, lane < static_cast<int>(p.R), pre_lo, pre_hi);
           pre_u = pred;
         }
       }

@@ -15,6 +15,43 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return min(n, rank * per), min(n, (rank + 1) * per)
 
 
+class Layout:
+    """S range shards x G = world / S query groups over `world` ranks (S divides world).
+
+    Rank r holds shard s = r % S (rows shard_range(n, S, s)) and answers query group g = r // S
+    (queries shard_range(nq, G, g)); the S ranks of a group -- g*S .. g*S + S - 1, neighbours on one
+    node -- exchange their per-shard top-k inside their own process group.  S = world is the
+    north star's pure base-range sharding (every rank sees every query), S = 1 pure query
+    splitting over whole-index replicas (no collective on the data path).  Each of the S shards is
+    held by G ranks; total work per step is fixed ("strong")."""
+
+    def __init__(self, world: int, rank: int, shards: int):
+        if shards < 1 or world % shards:
+            raise ValueError(f"shards ({shards}) must divide the number of ranks ({world})")
+        self.world, self.rank, self.shards = world, rank, shards
+        self.groups = world // shards
+        self.shard, self.group = rank % shards, rank // shards
+        self.group_ranks = list(range(self.group * shards, (self.group + 1) * shards))
+
+    def rows(self, n: int) -> tuple[int, int]:
+        return shard_range(n, self.shards, self.shard)
+
+    def queries(self, nq: int) -> tuple[int, int]:
+        return shard_range(nq, self.groups, self.group)
+
+    def new_groups(self, dist):
+        """Create every query group's process group (collective: every rank calls it, in the same
+        order) and return this rank's -- None when a group is the whole world (use the default)."""
+        if self.groups == 1:
+            return None
+        mine = None
+        for g in range(self.groups):
+            pg = dist.new_group(list(range(g * self.shards, (g + 1) * self.shards)))
+            if g == self.group:
+                mine = pg
+        return mine
+
+
 def merge_topk(all_ids, all_dists, k: int):
     """all_ids / all_dists: [nq, G*k] (torch).  Deterministic top-k by (dist, id)."""
     import torch
@@ -77,6 +114,10 @@ def exchange_packed(packed, k: int, group=None):
 
     world = dist.get_world_size(group)
     device = packed.device
+    if world == 1:  # a one-shard layout (S = 1): nothing to exchange, the sort gives the (dist, id) order
+        best = torch.sort(packed, dim=1).values[:, :k]
+        ids, d = unpack_candidates(best)
+        return ids, d
     if dist.get_backend(group) == "gloo" and device.type != "cpu":  # gloo gathers host tensors
         packed = packed.cpu()
     parts = [torch.empty_like(packed) for _ in range(world)]
@@ -283,3 +324,29 @@ class ShardedIndex:
         import torch
 
         return torch.device("cuda", self._device)
+
+
+def gather_layout_results(ids, dists, layout: Layout, nq: int, dist):
+    """Every query group's merged (ids, dists) -> the whole batch in query order, on every rank
+    (untimed: recall checks).  The ranks of a group hold the same merged rows; group g's rows come
+    from its first rank.  Slices are padded to ceil(nq / G) rows for the all_gather."""
+    import torch
+
+    per = (nq + layout.groups - 1) // layout.groups
+    dev = ids.device
+    if dist.get_backend() == "gloo" and dev.type != "cpu":
+        ids, dists = ids.cpu(), dists.cpu()
+    pi = torch.zeros((per, ids.shape[1]), dtype=torch.int64, device=ids.device)
+    pd = torch.zeros((per, ids.shape[1]), dtype=torch.float32, device=ids.device)
+    pi[:ids.shape[0]] = ids.to(torch.int64)
+    pd[:ids.shape[0]] = dists
+    gi = [torch.empty_like(pi) for _ in range(layout.world)]
+    gd = [torch.empty_like(pd) for _ in range(layout.world)]
+    dist.all_gather(gi, pi)
+    dist.all_gather(gd, pd)
+    out_i, out_d = [], []
+    for g in range(layout.groups):
+        a, b = shard_range(nq, layout.groups, g)
+        out_i.append(gi[g * layout.shards][:b - a])
+        out_d.append(gd[g * layout.shards][:b - a])
+    return torch.cat(out_i).to(dev), torch.cat(out_d).to(dev)

@@ -11,7 +11,10 @@ call; rank 0 prints the JSON line.  The workload is config 4 (10k queries) unles
   --mode shard   (default) base rows partitioned by range, one HNSW graph per shard, every rank
                  searches all queries on its shard, per-shard top-k exchanged with an RCCL
                  all_gather over xGMI and merged by (distance, global id).  Total work fixed:
-                 "scaling": "strong".
+                 "scaling": "strong".  --shards S (S divides N) runs S range shards x N/S query
+                 groups instead (sharded.Layout); by default the shard run is followed by a
+                 "layouts" leg measuring every other S (the S = 1 layout is SURVEY §8e's replica
+                 mode, queries split by range), reported beside `value` with the best of them.
   --mode replica every rank holds the whole index and answers its own 1k-query batch; no
                  collective on the data path: "scaling": "weak".
 
@@ -93,8 +96,13 @@ def parse():
     p.add_argument("--ef", type=int, default=0, help="fixed ef (skip the recall sweep)")
     p.add_argument("--target-recall", type=float, default=0.95)
     p.add_argument("--mode", choices=("shard", "replica"), default="shard")
-    p.add_argument("--no-replica-leg", action="store_true",
-                   help="N>1 shard mode: skip the replica-mode leg reported beside the shard result")
+    p.add_argument("--shards", type=int, default=0,
+                   help="N>1 shard mode: S range shards x N/S query groups (S divides N); 0 = N (every rank "
+                        "its own shard, every query on every rank: the north star's layout)")
+    p.add_argument("--layouts", default="auto",
+                   help="N>1 shard mode: other S to measure beside the result: 'auto' (every divisor of N), "
+                        "'none', or a comma list")
+    p.add_argument("--no-replica-leg", action="store_true", help="alias of --layouts none")
     p.add_argument("--build-threads", type=int, default=0)
     p.add_argument("--builder", choices=("auto", "host", "gpu"), default="auto",
                    help="graph builder: host = HNSWBuilder restated on the host (cached; multi-threaded, so "
@@ -221,14 +229,16 @@ def graph_for(native, base, efc, threads, cache_dir, tag, metric=0):
     return g, dt
 
 
-def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64, metric=0,
-             chunk=1_000_000):
-    """Exact top-k (L2, or IP = largest inner product): fp32 GEMM shortlist on the device, float64
-    re-rank on the host.  The base is scanned in chunks of `chunk` rows: one GEMM operand above 2^31
-    elements (e.g. 10M x 768) is outside what the BLAS kernels index correctly."""
+def exact_candidates(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64, metric=0,
+                     chunk=1_000_000):
+    """Exact top-k (L2, or IP = largest inner product) with their float64 distances: fp32 GEMM
+    shortlist on the device, float64 re-rank on the host (ties by id).  The base is scanned in chunks
+    of `chunk` rows: one GEMM operand above 2^31 elements (e.g. 10M x 768) is outside what the BLAS
+    kernels index correctly."""
     nq = queries_host.shape[0]
     n = base_dev.shape[0]
     out = np.zeros((nq, k), np.int64)
+    out_d = np.zeros((nq, k), np.float64)
     for s in range(0, nq, 256):
         q = queries_dev[s:s + 256]
         best_d, best_i = None, None
@@ -249,8 +259,17 @@ def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64
             x = base_host[c].astype(np.float64)
             y = queries_host[s + j].astype(np.float64)
             dd = ((x - y) ** 2).sum(1) if metric == 0 else -(x @ y)
-            out[s + j] = c[np.lexsort((c, dd))][:k]
-    return out
+            o = np.lexsort((c, dd))[:k]
+            m = len(o)
+            out[s + j, :m], out_d[s + j, :m] = c[o], dd[o]
+            if m < k:  # fewer rows than k
+                out[s + j, m:], out_d[s + j, m:] = -1, np.inf
+    return out, out_d
+
+
+def exact_gt(torch, base_dev, queries_dev, base_host, queries_host, k=K, cand=64, metric=0, chunk=1_000_000):
+    """Exact top-k ids (exact_candidates without the distances)."""
+    return exact_candidates(torch, base_dev, queries_dev, base_host, queries_host, k, cand, metric, chunk)[0]
 
 
 def f64_topk(base, ys, k=K, chunk=32768):
@@ -485,25 +504,36 @@ def main():
     dev = torch.device("cuda", local)
 
     from alayalite_amd import _native
-    from alayalite_amd.sharded import exchange_and_merge, shard_range, shard_search
+    from alayalite_amd.sharded import Layout, exchange_and_merge, gather_layout_results, shard_search
     import workloads.datasets as datasets
 
     native = _native._ext
     threads = args.build_threads or host_threads()
 
+    shard_mode = world > 1 and args.mode == "shard"
+    lay = Layout(world, rank, args.shards or world) if shard_mode else None
+    group = lay.new_groups(dist) if shard_mode else None
     t0 = time.time()
-    base, queries = getattr(datasets, w["gen"])(args.n, args.nq, args.dim)
-    log(f"data {base.shape} + {queries.shape} in {time.time() - t0:.1f}s")
+    if shard_mode and w["gen"] == "text_like":
+        # each rank generates only its shard's rows (config 5: 30.7 GB of f32 per whole base)
+        lo, hi = lay.rows(args.n)
+        base = None
+        my_base = datasets.text_like_rows(lo, hi, args.dim)
+        queries = datasets.text_like_queries(args.nq, args.dim)
+        log(f"data: rows [{lo}, {hi}) of {args.n} + {queries.shape} in {time.time() - t0:.1f}s")
+    else:
+        base, queries = getattr(datasets, w["gen"])(args.n, args.nq, args.dim)
+        log(f"data {base.shape} + {queries.shape} in {time.time() - t0:.1f}s")
+        if shard_mode:
+            lo, hi = lay.rows(args.n)
+            my_base = np.ascontiguousarray(base[lo:hi])
+        else:
+            lo, hi = 0, args.n
+            my_base = base
+    tag = (f"{w['gen']}_m{metric}_shard{lay.shard}of{lay.shards}" if shard_mode else
+           f"{w['gen']}_m{metric}" if w["gen"] != "gist_like" else "gist")
 
     # ---- index (shard or replica) ------------------------------------------------------------
-    if world > 1 and args.mode == "shard":
-        lo, hi = shard_range(args.n, world, rank)
-        my_base = np.ascontiguousarray(base[lo:hi])
-        tag = f"{w['gen']}_m{metric}_shard{rank}of{world}"
-    else:
-        lo, hi = 0, args.n
-        my_base = base
-        tag = f"{w['gen']}_m{metric}" if w["gen"] != "gist_like" else "gist"
     builder = args.builder if args.builder != "auto" else "gpu"
     index = native.DeviceIndex(local)
     index.set_base(my_base, metric)
@@ -525,14 +555,15 @@ def main():
         index.set_sq8(codes, mn, mx, order)
         sq8 = (codes, mn, mx, order)
 
-    q_dev = torch.from_numpy(queries).to(dev)
+    q_all = torch.from_numpy(queries).to(dev)
+    nq_total = q_all.shape[0]
+    qa, qb = lay.queries(nq_total) if shard_mode else (0, nq_total)
+    q_dev = q_all[qa:qb]  # this rank's query group (the whole batch unless --shards < N)
     nq = q_dev.shape[0]
     ids_dev = torch.empty((nq, K), dtype=torch.int32, device=dev)
     dists_dev = torch.empty((nq, K), dtype=torch.float32, device=dev)
     cnt_dev = torch.empty((nq, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
-
-    shard_mode = world > 1 and args.mode == "shard"
 
     def launch(ef, ix=None):
         ix = index if ix is None else ix
@@ -550,23 +581,29 @@ def main():
     def step(ef):
         launch(ef)
         if shard_mode:
-            return exchange_and_merge(ids_dev, dists_dev, lo, K)
+            return exchange_and_merge(ids_dev, dists_dev, lo, K, group)
         return ids_dev, dists_dev
 
     # ---- ground truth + operating point ------------------------------------------------------
     gt_check = None
-    if rank == 0:
+    gt = None
+    if base is None:  # rows generated per rank: every rank scores its own rows, rank 0 merges
+        gt = sharded_exact_gt(torch, dist, dev, my_base, lo, q_all, queries, metric, lay)
+        gt_check = "per-shard exact candidates merged on rank 0"
+    elif rank == 0:
         if metric == 0:
             gt, gt_check = exact_gt_flat(native, base, queries, local)
         else:  # IP (config 5): fp32 GEMM shortlist + float64 re-rank
             base_dev = torch.from_numpy(base).to(dev)
-            gt = exact_gt(torch, base_dev, q_dev, base, queries, metric=metric)
+            gt = exact_gt(torch, base_dev, q_all, base, queries, metric=metric)
             del base_dev
         torch.cuda.empty_cache()
 
     def probe(ef):
         """recall@10 >= target at this ef (decided on rank 0, broadcast to every rank)."""
-        ids, _ = step(ef)
+        ids, dd = step(ef)
+        if shard_mode and lay.groups > 1:  # every query group's merged rows, in query order
+            ids, dd = gather_layout_results(ids, dd, lay, nq_total, dist)
         torch.cuda.synchronize()
         ok = False
         if rank == 0:
@@ -601,7 +638,7 @@ def main():
             ev[i][1].record(stream)
             if shard_mode:
                 # exchange + merge of the same step (the search above is the per-shard kernel)
-                exchange_and_merge(ids_dev, dists_dev, lo, K)
+                exchange_and_merge(ids_dev, dists_dev, lo, K, group)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -631,8 +668,8 @@ def main():
         # above (search, then exchange, per step) is reported beside it with the exchange alone
         sync_elapsed = elapsed
         elapsed, pipe_search_ms = timed_pipeline(torch, dist, dev, ef, args.steps, args.warmup, index, lo, use_sq8,
-                                                 q_dev, nq)
-        exch_ms = timed_exchange(torch, dist, ids_dev, dists_dev, lo, args.steps)
+                                                 q_dev, nq, group)
+        exch_ms = timed_exchange(torch, dist, ids_dev, dists_dev, lo, args.steps, group)
         overlap = {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
                    "sync_ms_per_step": round(sync_elapsed / args.steps * 1e3, 4),
                    "search_ms": round(kernel_ms, 4), "search_ms_in_pipeline": round(pipe_search_ms, 4),
@@ -690,14 +727,20 @@ def main():
     # measured streaming-read ceiling of this GPU (reported beside the 8 TB/s vendor figure)
     measured_peak = native.hbm_stream_read(local, 4 << 30, 5) if rank == 0 else 0.0
 
-    units_per_step = nq * (world if (world > 1 and args.mode == "replica") else 1)
+    units_per_step = nq_total * (world if (world > 1 and args.mode == "replica") else 1)
     value = units_per_step * args.steps / elapsed
 
-    # ---- replica leg (N>1 shard mode): the whole index on every GPU, each rank its own batch ---
-    replica = None
-    if world > 1 and args.mode == "shard" and not args.no_replica_leg:
-        replica = replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, launch, rank, world,
-                              nq, ids_dev, stream, gt if rank == 0 else None)
+    # ---- layouts leg (N>1 shard mode): the other S-shard x N/S-query-group layouts -------------
+    layouts = None
+    if shard_mode and args.layouts != "none" and not args.no_replica_leg:
+        others = ([s_ for s_ in range(1, world + 1) if world % s_ == 0 and s_ != lay.shards]
+                  if args.layouts == "auto" else [int(x) for x in args.layouts.split(",")])
+        layouts = []
+        for S in others:
+            row = layout_leg(args, native, torch, dist, dev, S, base, metric, use_sq8, threads, q_all, queries,
+                             rank, world, gt)
+            if row is not None:
+                layouts.append(row)
 
     # ---- CPU baseline: the reference's coroutine batch_search restated (oracle/) --------------
     cpu = None
@@ -708,7 +751,7 @@ def main():
     if rank == 0:
         r_at = next((s["recall"] for s in sweep if s["ef"] == ef), None)
         out = {
-            "metric": metric_label(w, args.n, nq),
+            "metric": metric_label(w, args.n, nq_total),
             "value": round(value, 1),
             "unit": "queries/s",
             "n_gpus": world,
@@ -721,10 +764,15 @@ def main():
             "dtype": "u8+f32" if use_sq8 else "f32",
             "data": w["data"] + ("; graph from the device HNSW build" if builder == "gpu" else ""),
             "config": {"workload": f"hnsw-{w['gen'].split('_')[0]}{args.dim}-{args.n // 1000}k-"
-                                   f"{'ip-sq8' if use_sq8 else ('ip' if metric else 'l2')}-{nq}q",
-                       "n_base": args.n, "n_queries": nq, "dim": args.dim, "k": K, "ef_search": ef,
+                                   f"{'ip-sq8' if use_sq8 else ('ip' if metric else 'l2')}-{nq_total}q",
+                       "n_base": args.n, "n_queries": nq_total, "dim": args.dim, "k": K, "ef_search": ef,
                        "recall_at_10": r_at, "ef_sweep": sweep, "mode": args.mode if world > 1 else "single",
-                       "parallelism": f"{args.mode}{world}" if world > 1 else "1gpu",
+                       "parallelism": (f"{lay.shards}shards-x-{lay.groups}querygroups" if shard_mode else
+                                       f"{args.mode}{world}" if world > 1 else "1gpu"),
+                       "timed_region": ("device-resident queries and results: the search launches (plus the "
+                                        "exchange when N > 1) between synchronised barriers, as the task contract "
+                                        "defines value; SURVEY 8d's host-buffer region (H2D queries + search + "
+                                        "D2H ids/distances) is pcie_inclusive"),
                        "graph_build_s": round(build_s, 1), "graph_builder": builder,
                        "ground_truth": ("engine flat path (f32 metric of find_exact_gt), float64 top-10 sets "
                                         f"equal on {gt_check} sampled queries") if gt_check else
@@ -747,8 +795,14 @@ def main():
         }
         if curve is not None:
             out["config"]["qps_curve"] = curve
-        if replica is not None:
-            out["replica"] = replica
+        if layouts is not None:
+            out["layouts"] = layouts
+            if layouts:
+                best = max(layouts + [{"shards": lay.shards, "query_groups": lay.groups, "value": round(value, 1)}],
+                           key=lambda x: x["value"])
+                out["best_layout"] = {"shards": best["shards"], "query_groups": best["query_groups"],
+                                      "value": best["value"],
+                                      "note": "value stays the north star's layout; this is the fastest measured"}
         if overlap is not None:
             out["exchange_overlap"] = overlap
         if pcie is not None:
@@ -758,14 +812,14 @@ def main():
         dist.destroy_process_group()
 
 
-def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_dev, nq):
+def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_dev, nq, group=None):
     """K shard steps through ShardPipeline (double-buffered: the search of step i+1 overlaps the
     exchange of step i); barrier + synchronize on both sides, max over ranks.  Returns (seconds,
     mean search ms inside the pipeline, from a second untimed pass with events)."""
     from alayalite_amd.sharded import ShardPipeline, shard_search
 
     fn = lambda q, i, d, c, s: shard_search(index, lo, use_sq8, q, K, ef, i, d, c, s)  # noqa: E731
-    pipe = ShardPipeline(fn, nq, K, lo, dev)
+    pipe = ShardPipeline(fn, nq, K, lo, dev, group)
     pipe.run([q_dev] * max(1, warmup))
     torch.cuda.synchronize()
     dist.barrier()
@@ -777,7 +831,7 @@ def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_de
     el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # the search time as it runs inside the pipeline (a separate, untimed pass with events)
-    tp = ShardPipeline(fn, nq, K, lo, dev, timing=True)
+    tp = ShardPipeline(fn, nq, K, lo, dev, group, timing=True)
     tp.run([q_dev] * steps)
     torch.cuda.synchronize()
     sm = torch.tensor([tp.search_ms()], device=dev, dtype=torch.float64)
@@ -785,45 +839,78 @@ def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_de
     return el.item(), sm.item()
 
 
-def timed_exchange(torch, dist, ids_dev, dists_dev, lo, steps):
+def timed_exchange(torch, dist, ids_dev, dists_dev, lo, steps, group=None):
     """The exchange alone (pack, all_gather, merge sort) on resident shard results: ms per step,
     max over ranks."""
     from alayalite_amd.sharded import exchange_and_merge
 
-    exchange_and_merge(ids_dev, dists_dev, lo, K)
+    exchange_and_merge(ids_dev, dists_dev, lo, K, group)
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        exchange_and_merge(ids_dev, dists_dev, lo, K)
+        exchange_and_merge(ids_dev, dists_dev, lo, K, group)
     torch.cuda.synchronize()
     el = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], device=ids_dev.device, dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     return el.item()
 
 
-def replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, launch, rank, world, nq,
-                ids_dev, stream, gt):
-    """SURVEY §8e replica mode, reported beside shard mode: every rank holds the whole index (graph
-    from the device build) and answers its own batch; no collective on the data path.  The
-    operating ef is chosen on rank 0 against the same ground truth.  value = world * nq / step time
-    (max over ranks): "scaling": "weak"."""
+# host bytes of one rank's shard rows beyond which a layouts leg is skipped (the S = 1 layout of config
+# 5 would hold the whole 30.7 GB f32 base on every rank)
+LAYOUT_ROWS_CAP_BYTES = 16 << 30
+
+
+def layout_leg(args, native, torch, dist, dev, S, base, metric, use_sq8, threads, q_all, queries, rank, world, gt):
+    """One S-shard x N/S-query-group layout (sharded.Layout) beside the main result: rank r builds
+    shard r % S on the device (SQ8: its own quantizer; the shard holding global row 0 keeps the
+    rerank's id-0 entries) and answers query group r // S; the group's ranks exchange inside their
+    own process group.  The operating ef is chosen on rank 0 against the same ground truth.  S = 1
+    is SURVEY §8e's replica mode (whole index per GPU, queries split by range, no collective).
+    value = all queries x steps / step time (max over ranks): total work fixed ("strong")."""
+    from alayalite_amd.sharded import Layout, exchange_and_merge, gather_layout_results, shard_search
+    import workloads.datasets as datasets
+
+    lay = Layout(world, rank, S)
+    group = lay.new_groups(dist)
+    lo, hi = lay.rows(args.n)
+    if (hi - lo) * args.dim * 4 > LAYOUT_ROWS_CAP_BYTES:
+        log(f"layout {S}x{lay.groups}: skipped ({hi - lo} rows of {args.dim} f32 per rank)")
+        return None
     t = time.time()
-    full = native.DeviceIndex(dev.index)
-    full.set_base(base, metric)
-    full.build_graph(R, args.efc, 100, 0, 0, 2)
+    rows = np.ascontiguousarray(base[lo:hi]) if base is not None else datasets.text_like_rows(lo, hi, args.dim)
+    ix = native.DeviceIndex(dev.index)
+    ix.set_base(rows, metric)
+    ix.build_graph(R, args.efc, 100, 0, 0, 2)
     if use_sq8:
-        mn, mx = native.sq8_train(base)
-        full.set_sq8(native.sq8_encode(base, mn, mx, threads), mn, mx, native.host_sq8_order())
-    log(f"replica leg: device-built full graph in {time.time() - t:.1f}s")
+        mn, mx = native.sq8_train(rows)
+        ix.set_sq8(native.sq8_encode(rows, mn, mx, threads), mn, mx, native.host_sq8_order())
+    del rows
+    nq_total = q_all.shape[0]
+    qa, qb = lay.queries(nq_total)
+    q = q_all[qa:qb]
+    nq = q.shape[0]
+    ids = torch.empty((nq, K), dtype=torch.int32, device=dev)
+    dd = torch.empty((nq, K), dtype=torch.float32, device=dev)
+    cnt = torch.empty((nq, 4), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    dist.barrier()
+    log(f"layout {S}x{lay.groups}: shard graphs built in {time.time() - t:.1f}s")
+
+    def step(ef):
+        shard_search(ix, lo, use_sq8, q, K, ef, ids, dd, cnt, stream.cuda_stream)
+        return exchange_and_merge(ids, dd, lo, K, group)
+
     sweep = []
 
     def probe(ef):
-        launch(ef, full)
+        mi, md = step(ef)
+        if lay.groups > 1:
+            mi, md = gather_layout_results(mi, md, lay, nq_total, dist)
         torch.cuda.synchronize()
         ok = False
         if rank == 0:
-            r = recall(ids_dev.cpu().numpy(), gt)
+            r = recall(mi.cpu().numpy(), gt)
             sweep.append({"ef": ef, "recall": round(r, 4)})
             ok = r >= args.target_recall
         flag = torch.tensor([1 if ok else 0], device=dev)
@@ -832,22 +919,57 @@ def replica_leg(args, native, torch, dist, dev, base, metric, use_sq8, threads, 
 
     ef = choose_ef(probe)
     for _ in range(args.warmup):
-        launch(ef, full)
+        step(ef)
+    torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        launch(ef, full)
+        step(ef)
     torch.cuda.synchronize()
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = el.item()
-    r_at = next((s["recall"] for s in sweep if s["ef"] == ef), None)
-    out = {"value": round(world * nq * args.steps / el, 1), "unit": "queries/s", "scaling": "weak",
-           "ms_per_step": round(el / args.steps * 1e3, 4), "ef_search": ef, "recall_at_10": r_at,
-           "graph_builder": "gpu", "note": "whole index on every GPU, each rank its own batch, no collective"}
-    log("replica leg", out)
+    r_at = next((x["recall"] for x in sweep if x["ef"] == ef), None)
+    out = {"shards": S, "query_groups": lay.groups, "value": round(nq_total * args.steps / el, 1),
+           "unit": "queries/s", "scaling": "strong", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "ef_search": ef, "recall_at_10": r_at, "graph_builder": "gpu",
+           "note": ("whole index per GPU, queries split by range, no collective (SURVEY 8e replica mode)" if S == 1
+                    else f"{S} range shards, {lay.groups} query groups all-gathering inside their own process group")}
+    log("layout", out)
+    del ix
+    torch.cuda.empty_cache()
+    return out
+
+
+def sharded_exact_gt(torch, dist, dev, rows, lo, q_all, queries, metric, lay, k=K):
+    """Exact top-k when no rank holds the whole base (rows generated per rank): every rank scores its
+    own rows (exact_candidates: fp32 GEMM shortlist, float64 re-rank), the per-shard (float64
+    distance, global id) candidates are gathered, and rank 0 keeps the k smallest by (distance, id).
+    Returns the ids on rank 0, None elsewhere."""
+    base_dev = torch.from_numpy(rows).to(dev)
+    ids, d64 = exact_candidates(torch, base_dev, q_all, rows, queries, k=k, metric=metric)
+    del base_dev
+    torch.cuda.empty_cache()
+    ids = torch.from_numpy(ids + lo).to(dev)
+    d64 = torch.from_numpy(d64).to(dev)
+    gi = [torch.empty_like(ids) for _ in range(lay.world)]
+    gd = [torch.empty_like(d64) for _ in range(lay.world)]
+    if dist.get_backend() == "gloo":
+        ids, d64 = ids.cpu(), d64.cpu()
+        gi = [x.cpu() for x in gi]
+        gd = [x.cpu() for x in gd]
+    dist.all_gather(gi, ids)
+    dist.all_gather(gd, d64)
+    if lay.rank != 0:
+        return None
+    # shard r % S holds rows lay.rows(); every shard appears G times (query groups): take one copy each
+    ai = np.concatenate([gi[s].cpu().numpy() for s in range(lay.shards)], 1)
+    ad = np.concatenate([gd[s].cpu().numpy() for s in range(lay.shards)], 1)
+    out = np.zeros((ai.shape[0], k), np.int64)
+    for qi in range(ai.shape[0]):
+        out[qi] = ai[qi][np.lexsort((ai[qi], ad[qi]))][:k]
     return out
 
 
@@ -886,10 +1008,14 @@ def cpu_baseline(args, graph, base, queries, ef, metric, sq8, device_ids):
     med = float(np.median(runs))
     parity = bool(np.array_equal(cpu_ids, device_ids[:m]))
     what = "search + rerank" if sq8 is not None else "search"
+    qps = sorted(m / r for r in runs)
     return {"value": round(m / med, 1), "unit": "queries/s", "cores": ct, "kind": "port",
             "sample": f"{m} of {nq} queries at ef={ef} ({what}), median of {len(runs)} runs after 1 warm-up "
                       f"(Scheduler begin->join{' + rerank loop' if sq8 is not None else ''}), "
                       f"ids_equal_to_device={parity}",
+            "spread": {"runs": len(runs), "min": round(qps[0], 1), "median": round(m / med, 1),
+                       "max": round(qps[-1], 1), "note": "queries/s per timed run (the host is shared: "
+                                                         "runs of different rounds differ up to ~2x)"},
             "host": host_info()}
 
 

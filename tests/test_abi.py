@@ -33,3 +33,25 @@ def test_no_device_fails_loudly(native):
 
     with pytest.raises(RuntimeError, match="no HIP device"):
         native.DeviceIndex(0)
+
+
+def test_import_starts_no_gpu_runtime():
+    """Importing the package loads torch's libraries (so the engine's HIP soname resolves to the
+    runtime torch uses) but calls nothing on the device: torch.cuda.is_available() is never called
+    and torch stays uninitialised (a fork or exec after import must stay safe)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import torch, torch.cuda\n"
+        "calls = []\n"
+        "real = torch.cuda.is_available\n"
+        "torch.cuda.is_available = lambda *a, **k: calls.append(1) or real(*a, **k)\n"
+        "import alayalite_amd\n"
+        "assert calls == [], calls\n"
+        "assert not torch.cuda.is_initialized()\n"
+        "print('ok')\n")
+    env = dict(os.environ)
+    env.pop("ALAYA_SKIP_TORCH_INIT", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

@@ -182,3 +182,74 @@ def test_shard_pipeline_gloo(tmp_path):
             parts.append((ids.numpy(), d.numpy()))
         ref_i, ref_d = merge_reference([p[0] for p in parts], [p[1] for p in parts], [0, 300], 10)
         assert np.array_equal(got["over_i"][b], ref_i) and np.array_equal(got["over_d"][b], ref_d)
+
+
+def _layout_worker(rank, world, port, out_path, shards):
+    """S shards x (world / S) query groups: rank r searches its group's query slice on its shard
+    (exact top-k stand-in), the group's ranks exchange inside their own process group, and every
+    group's merged rows are gathered back into query order."""
+    import torch.distributed as dist
+
+    from alayalite_amd.sharded import Layout, exchange_and_merge, gather_layout_results
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lay = Layout(world, rank, shards)
+    group = lay.new_groups(dist)
+    base, queries = _layout_data()
+    lo, hi = lay.rows(base.shape[0])
+    qa, qb = lay.queries(queries.shape[0])
+    rows = base[lo:hi]
+    q = queries[qa:qb]
+    dd = ((q[:, None, :] - rows[None, :, :]) ** 2).sum(-1).astype(np.float32)
+    o = np.stack([np.lexsort((np.arange(rows.shape[0]), r))[:10] for r in dd])
+    ids, d = torch.from_numpy(o.astype(np.int32)), torch.from_numpy(np.take_along_axis(dd, o, 1))
+    mi, md = exchange_and_merge(ids, d, lo, 10, group)
+    gi, gd = gather_layout_results(mi, md, lay, queries.shape[0], dist)
+    if rank == 0:
+        np.savez(out_path, ids=gi.numpy(), d=gd.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _layout_data():
+    rng = np.random.default_rng(11)
+    return rng.random((601, 6), dtype=np.float32), rng.random((29, 6), dtype=np.float32)
+
+
+@pytest.mark.parametrize("shards", [2, 1, 4])
+def test_shards_by_query_groups_gloo(tmp_path, shards):
+    """world 4 as 2 shards x 2 query groups (and 1 x 4, 4 x 1): the merged result of every query
+    equals merge_reference over the per-shard exact top-k, and -- the stand-in search being exact --
+    the exact top-k of the whole base by (distance, id)."""
+    import torch.multiprocessing as mp
+
+    from alayalite_amd.sharded import merge_reference, shard_range
+
+    out = str(tmp_path / "layout.npz")
+    mp.spawn(_layout_worker, args=(4, _free_port(), out, shards), nprocs=4, join=True)
+    got = np.load(out)
+    base, queries = _layout_data()
+    parts, offs = [], []
+    for s in range(shards):
+        lo, hi = shard_range(base.shape[0], shards, s)
+        dd = ((queries[:, None, :] - base[None, lo:hi, :]) ** 2).sum(-1).astype(np.float32)
+        o = np.stack([np.lexsort((np.arange(hi - lo), r))[:10] for r in dd])
+        parts.append((o.astype(np.int32), np.take_along_axis(dd, o, 1)))
+        offs.append(lo)
+    ref_i, ref_d = merge_reference([p[0] for p in parts], [p[1] for p in parts], offs, 10)
+    assert np.array_equal(got["ids"], ref_i) and np.array_equal(got["d"], ref_d)
+    full = ((queries[:, None, :] - base[None, :, :]) ** 2).sum(-1).astype(np.float32)
+    exact = np.stack([np.lexsort((np.arange(base.shape[0]), r))[:10] for r in full])
+    assert np.array_equal(got["ids"], exact)
+
+
+def test_layout_rank_map():
+    from alayalite_amd.sharded import Layout
+
+    lays = [Layout(8, r, 2) for r in range(8)]
+    assert [(x.shard, x.group) for x in lays] == [(r % 2, r // 2) for r in range(8)]
+    assert lays[5].group_ranks == [4, 5] and lays[5].queries(10000) == (5000, 7500)
+    assert Layout(8, 3, 8).queries(10000) == (0, 10000) and Layout(8, 3, 1).rows(100) == (0, 100)
+    with pytest.raises(ValueError):
+        Layout(8, 0, 3)

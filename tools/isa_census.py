@@ -148,6 +148,7 @@ def census(name: str, body: list[str]) -> dict:
                 "insts": len(ins),
                 "restores": sum(1 for s in ins if is_restore(s)),
                 "spill_stores": sum(1 for s in ins if is_spill(s)),
+                "scratch_ops": sum(1 for s in ins if s.startswith(("scratch_", "buffer_store", "buffer_load"))),
                 "valu": sum(1 for s in ins if s.startswith("v_")),
                 "salu": sum(1 for s in ins if s.startswith("s_") and not s.startswith(("s_waitcnt", "s_nop", "s_cbranch", "s_branch"))),
             }
@@ -159,6 +160,8 @@ def census(name: str, body: list[str]) -> dict:
         "restores_total": sum(1 for _, s in insts if is_restore(s)),
         "expansion_loops": loops,
         "restores_in_expansion_loops": sum(v["restores"] for v in loops.values()),
+        "scratch_ops_total": sum(1 for _, s in insts if s.startswith(("scratch_", "buffer_store", "buffer_load"))),
+        "scratch_ops_in_expansion_loops": sum(v["scratch_ops"] for v in loops.values()),
     }
 
 
@@ -180,6 +183,7 @@ def main() -> None:
         print(f"{r['kernel']:<44} scratch {r.get('ScratchSize', '?'):>3} sgpr {r.get('TotalNumSgprs', '?'):>3} vgpr {r.get('NumVgprs', '?'):>3} "
               f"occ {r.get('Occupancy', '?')}  spill slots {r['spill_slots']:>2}  restores {r['restores_total']:>3} "
               f"(in expansion loops: {r['restores_in_expansion_loops']}; loops {len(r['expansion_loops'])}, "
+              f"scratch ops {r['scratch_ops_total']} / in loops {r['scratch_ops_in_expansion_loops']}, "
               f"insts {sum(v['insts'] for v in r['expansion_loops'].values())})")
     if args.out:
         os.makedirs(os.path.dirname(args.out), exist_ok=True)

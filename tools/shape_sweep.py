@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--visited", default="0", help="visited-table layouts: 0 auto, 1 compact, 2 wide")
     ap.add_argument("--max-waves", default="0", help="caps on resident searchers per CU (ALAYA_MAX_WAVES_PER_CU); 0 = none")
     ap.add_argument("--table", default="0", help="slots per ef targets (0 = default policy); negative = fixed log2")
+    ap.add_argument("--spill-table", default="d",
+                    help="ALAYA_SPILL_TABLE values: d = the engine's default, 0 = bitset second level, 6..16 = log2 entries")
     ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     import torch
@@ -61,8 +63,11 @@ def main():
         ids = torch.empty((nq, 10), dtype=torch.int32, device="cuda")
         dd = torch.empty((nq, 10), dtype=torch.float32, device="cuda")
         cnt = torch.empty((nq, 4), dtype=torch.int32, device="cuda")
-        for w, mw, vm in [(w, mw, vm) for w in args.waves.split(",") for mw in args.max_waves.split(",")
-                          for vm in args.visited.split(",")]:
+        for w, mw, vm, stb in [(w, mw, vm, stb) for w in args.waves.split(",") for mw in args.max_waves.split(",")
+                               for vm in args.visited.split(",") for stb in args.spill_table.split(",")]:
+            os.environ.pop("ALAYA_SPILL_TABLE", None)
+            if stb != "d":
+                os.environ["ALAYA_SPILL_TABLE"] = stb
             dev.set_visited_mode(int(vm))
             os.environ.pop("ALAYA_SEARCH_WAVES", None)
             if w != "0":
@@ -97,10 +102,11 @@ def main():
                 ms = e0.elapsed_time(e1) / args.reps
                 h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
                 c = cnt.cpu().numpy()
-                print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
+                print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb} spill-table {stb}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
                       f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}", flush=True)
     os.environ.pop("ALAYA_SEARCH_WAVES", None)
     os.environ.pop("ALAYA_MAX_WAVES_PER_CU", None)
+    os.environ.pop("ALAYA_SPILL_TABLE", None)
 
 
 if __name__ == "__main__":

@@ -1,13 +1,18 @@
-"""One-GPU rehearsal of bench.py --mode shard at G = 1, 2, 4, 8 (8-GPU runs are the driver's).
+"""One-GPU rehearsal of bench.py's N-GPU shard layouts (8-GPU runs are the driver's).
 
-For each G: build the G base-range shard graphs on the device exactly as bench.py's ranks do
-(alaya_index_build_graph, deterministic), search
-every shard on this GPU in turn, merge the per-shard top-k by (dist, global id) with the same
-merge the ranks use, pick the smallest ef of the sweep whose merged recall@10 >= 0.95, and time
-each shard's kernel at that ef.  Predicted G-GPU QPS = nq / max over shards of the kernel time
-(the all-gather of nq*k*8 B per rank and the merge are measured separately by bench.py).
+Layout S x G (sharded.Layout): S base-range shards, G = N / S query groups; rank r holds shard r % S
+and answers query group r // S (nq / G queries), exchanging inside its group.  S = N is the north
+star's pure sharding, S = 1 replicas with the queries split by range.  For each S: build the S shard
+graphs on the device exactly as the ranks do (alaya_index_build_graph, deterministic; SQ8: each
+shard's own quantizer, the rerank's id-0 entries on the shard holding global row 0), search every
+shard on this GPU, merge the per-shard top-k by (dist, global id), pick the smallest ef of the sweep
+whose merged recall@10 >= 0.95, then time every (shard, query group) pair a rank would run at that
+ef.  Predicted N-GPU QPS = nq / the slowest pair's kernel time (the exchange -- nq/G x k x 8 B per
+rank -- is measured by bench.py); efficiency = predicted / (N x the one-GPU QPS of the whole index
+on the whole batch at its own ef).
 
-usage: python tools/shard_rehearsal.py [--n 1000000] [--nq 10000] [--gs 1,2,4,8]   (config 4: 10k queries)
+usage: python tools/shard_rehearsal.py [--workload gist|sq8] [--n N] [--nq 10000] [--world 8] [--shards 1,2,4,8]
+       (config 4: gist, 1M, 10k queries; config 5: sq8, 10M x 768 IP SQ8 + rerank, 10k queries)
 """
 
 import argparse
@@ -24,87 +29,111 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--workload", choices=("gist", "sq8"), default="gist")
+    ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--nq", type=int, default=10000)
-    ap.add_argument("--dim", type=int, default=960)
-    ap.add_argument("--gs", default="1,2,4,8")
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--shards", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
 
     import bench as b
     from alayalite_amd import _native
-    from alayalite_amd.sharded import merge_reference, shard_range
-    from workloads.datasets import gist_like
+    from alayalite_amd.sharded import merge_reference, shard_range, shard_search
+    import workloads.datasets as ds
 
     ext = _native._ext
     dev = torch.device("cuda", 0)
-    base, queries = gist_like(args.n, args.nq, args.dim)
-    q_dev = torch.from_numpy(queries).to(dev)
-    gt, _ = b.exact_gt_flat(ext, base, queries, 0)
+    sq8 = args.workload == "sq8"
+    n = args.n or (10_000_000 if sq8 else 1_000_000)
+    metric = 1 if sq8 else 0
+    t = time.time()
+    base, queries = (ds.text_like(n, args.nq) if sq8 else ds.gist_like(n, args.nq, 960))
+    print(f"data {base.shape} in {time.time() - t:.1f}s", flush=True)
+    q_all = torch.from_numpy(queries).to(dev)
+    t = time.time()
+    if sq8:
+        base_dev = torch.from_numpy(base).to(dev)
+        gt = b.exact_gt(torch, base_dev, q_all, base, queries, metric=1)
+        del base_dev
+    else:
+        gt, _ = b.exact_gt_flat(ext, base, queries, 0)
     torch.cuda.empty_cache()
+    print(f"ground truth in {time.time() - t:.1f}s", flush=True)
     nq, K = args.nq, b.K
+    stream = torch.cuda.current_stream(dev)
+    order = ext.host_sq8_order()
+
+    def build(lo, hi):
+        rows = np.ascontiguousarray(base[lo:hi])
+        ix = ext.DeviceIndex(0)
+        ix.set_base(rows, metric)
+        ix.build_graph(b.R, 100, 100, 0, 0, 2)
+        if sq8:
+            mn, mx = ext.sq8_train(rows)
+            ix.set_sq8(ext.sq8_encode(rows, mn, mx, 16), mn, mx, order)
+        return ix
+
+    def search(ix, lo, q, ef, timed=False):
+        m = q.shape[0]
+        ids = torch.empty((m, K), dtype=torch.int32, device=dev)
+        dd = torch.empty((m, K), dtype=torch.float32, device=dev)
+        cnt = torch.empty((m, 4), dtype=torch.int32, device=dev)
+        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        shard_search(ix, lo, sq8, q, K, ef, ids, dd, cnt, stream.cuda_stream)
+        e.record(stream)
+        torch.cuda.synchronize()
+        return ids.cpu().numpy().astype(np.int64), dd.cpu().numpy().copy(), a.elapsed_time(e)
+
     results = []
-    for G in [int(x) for x in args.gs.split(",")]:
-        shards = []
-        for r in range(G):
-            lo, hi = shard_range(args.n, G, r)
-            sb = np.ascontiguousarray(base[lo:hi])
-            ix = ext.DeviceIndex(0)
-            ix.set_base(sb, 0)
-            t = time.time()
-            ix.build_graph(b.R, 100, 100, 0, 0, 2)
-            shards.append((lo, ix))
-            print(f"G={G} shard {r}: rows [{lo},{hi}) device graph {time.time() - t:.1f}s", flush=True)
-        ids = torch.empty((nq, K), dtype=torch.int32, device=dev)
-        dd = torch.empty((nq, K), dtype=torch.float32, device=dev)
-        cnt = torch.empty((nq, 4), dtype=torch.int32, device=dev)
-        stream = torch.cuda.current_stream(dev)
-
-        def search_all(ef, timed=False):
-            per_ids, per_d, times = [], [], []
-            for lo, ix in shards:
-                a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record(stream)
-                ix.shard_search_device(q_dev.data_ptr(), nq, K, ef, ids.data_ptr(), dd.data_ptr(), cnt.data_ptr(),
-                                       stream.cuda_stream)
-                e.record(stream)
-                torch.cuda.synchronize()
-                times.append(a.elapsed_time(e))
-                per_ids.append(ids.cpu().numpy().astype(np.int64))
-                per_d.append(dd.cpu().numpy().copy())
-            return per_ids, per_d, times
-
+    for S in [int(x) for x in args.shards.split(",")]:
+        G = args.world // S
+        spans = [shard_range(n, S, s) for s in range(S)]
+        t = time.time()
+        shards = [(lo, build(lo, hi)) for lo, hi in spans]
+        print(f"S={S}: {S} shard graphs in {time.time() - t:.1f}s", flush=True)
         sweep = []
 
         def probe(ef):
-            per_ids, per_d, _ = search_all(ef)
-            mi, _ = merge_reference(per_ids, per_d, [lo for lo, _ in shards], K)
+            per = [search(ix, lo, q_all, ef) for lo, ix in shards]
+            mi, _ = merge_reference([p[0] for p in per], [p[1] for p in per], [lo for lo, _ in shards], K)
             r = b.recall(mi, gt)
             sweep.append({"ef": ef, "recall": round(r, 4)})
             return r >= 0.95
 
-        chosen = b.choose_ef(probe)
-        search_all(chosen)  # warm
+        ef = b.choose_ef(probe)
+        groups = [shard_range(nq, G, g) for g in range(G)]
+        for lo, ix in shards:  # warm
+            search(ix, lo, q_all[groups[0][0]:groups[0][1]], ef)
         worst = []
         for _ in range(args.steps):
-            _, _, times = search_all(chosen)
-            worst.append(max(times))
+            worst.append(max(search(ix, lo, q_all[qa:qb], ef)[2] for lo, ix in shards for qa, qb in groups))
         ms = float(np.median(worst))
-        row = {"G": G, "ef": chosen, "recall": next(x["recall"] for x in sweep if x["ef"] == chosen), "max_shard_kernel_ms": round(ms, 3),
+        row = {"shards": S, "query_groups": G, "ef": ef, "recall": next(x["recall"] for x in sweep if x["ef"] == ef),
+               "queries_per_rank": groups[0][1] - groups[0][0], "max_rank_kernel_ms": round(ms, 3),
                "predicted_qps": round(nq / (ms * 1e-3), 1), "sweep": sweep}
+        if S == 1:  # the one-GPU reference: the whole index, the whole batch
+            whole = [search(shards[0][1], 0, q_all, ef)[2] for _ in range(args.steps)]
+            row["one_gpu_qps"] = round(nq / (float(np.median(whole)) * 1e-3), 1)
         results.append(row)
         print(json.dumps(row), flush=True)
         del shards
         torch.cuda.empty_cache()
-    base_qps = results[0]["predicted_qps"]
+    one = next((r["one_gpu_qps"] for r in results if "one_gpu_qps" in r), None)
     for r in results:
-        r["predicted_efficiency"] = round(r["predicted_qps"] / (r["G"] * base_qps), 3)
-    print(json.dumps(results))
+        if one:
+            r["predicted_efficiency"] = round(r["predicted_qps"] / (args.world * one), 3)
+    out = {"workload": args.workload, "n": n, "nq": nq, "world": args.world, "one_gpu_qps": one, "layouts": results,
+           "note": "kernel-only prediction on one MI355X: every (shard, query group) pair a rank runs, timed in turn; "
+                   "the exchange is not included"}
+    print(json.dumps(out), flush=True)
     if args.out:
+        os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as f:
-            json.dump(results, f, indent=1)
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
