@@ -211,11 +211,16 @@ constexpr uint32_t kDirtyCap = 16384;  // per-slot dirty-word list (64 KB): word
 // hash's low L - (s - 3) bits) fits 16 bits; at most 2^16 (128 KB per slot; ids wider than 28 bits
 // keep the bitset).  ALAYA_SPILL_TABLE=0 keeps the bitset, a value 6..16 forces the size (tests: tiny
 // tables fill their buckets and exercise the bitset fallback).
-uint32_t spill_table_log2(int sq8_order, uint32_t L, uint32_t ef) {
-  // f32 kernels: their tables rarely spill, they keep the bitset; so do the AVX2-order SQ8 kernels
-  // (hosts without AVX-512), whose SGPR budget the table's state would overrun (65-116 restores per
-  // expansion)
-  if (sq8_order != 2) return 0;
+uint32_t spill_table_log2(int sq8_order, uint32_t L, uint32_t ef, uint32_t dim = 0) {
+  // The AVX2-order SQ8 kernels (hosts without AVX-512) keep the bitset: the table's state would
+  // overrun their SGPR budget (65-116 restores per expansion).  f32 kernels: their tables rarely
+  // spill, they keep the bitset unless ALAYA_SPILL_TABLE_F32=1 (narrow rows, dim <= 256 in 32s:
+  // an experiment with the LDS first level bypassed)
+  if (sq8_order == 1) return 0;
+  if (sq8_order == 0) {
+    const char *f = std::getenv("ALAYA_SPILL_TABLE_F32");
+    if (!(f && f[0] == '1') || dim == 0 || dim > 256 || dim % 32 != 0) return 0;
+  }
   uint32_t s = std::max<uint32_t>({6u, ceil_log2(32ull * ef), L > 12 ? L - 12 : 0u});
   if (const char *e = std::getenv("ALAYA_SPILL_TABLE")) {
     const uint32_t v = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
@@ -248,10 +253,10 @@ void prepare_spill(alaya_index *ix, SearchParams &p, uint64_t slots, hipStream_t
   p.dirty_words = ix->dirty.as<uint32_t>();
   p.dirty_cap = cap;
   p.spill_table = nullptr;
-  p.stab_log2 = p.stab_rbits = 0;
+  p.stab_rbits = 0;
   p.spill_flags = 0;
   if (const char *e = std::getenv("ALAYA_SPILL_FLAGS")) p.spill_flags = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
-  if (const uint32_t st = spill_table_log2(p.sq8_order, p.vis_lbits, p.ef)) {
+  if (const uint32_t st = p.stab_log2) {
     const size_t tbytes = static_cast<size_t>(std::max<uint64_t>(slots, 1)) * (2ull << st);
     if (tbytes > ix->stab.bytes) {
       ix->stab.reserve(tbytes);
@@ -292,7 +297,7 @@ int search_waves(const SearchParams &p) {
 constexpr uint32_t kMaxCompactRbits = 11;
 // At most 4 searchers per SIMD: a 5th wave (the 96-VGPR d = 128 L2 kernel admits 5) halves every
 // table and costs more in probes than it hides -- SIFT 1M, 10k queries, ef 70: 16 waves per CU with
-// 4096-slot tables 1.198 ms, 20 with 2048-slot tables 1.513 ms (profiles/r03/sweeps/sift_max_waves.log);
+// 4096-slot tables 1.198 ms, 20 with 2048-slot tables 1.513 ms (profiles/r03/sift_c3/residency_sweep_tree.log);
 // config 5 measured 12 and 16 per CU equal.
 constexpr uint64_t kMaxSearchWavesPerCu = 16;
 uint64_t max_search_waves_per_cu() {
@@ -317,6 +322,10 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
       // probe past max_disp spills by itself
       p.vis_limit = static_cast<uint32_t>(std::max<uint64_t>(64, std::min<uint64_t>(lim, slots - 64)));
     }
+    if (const char *e = std::getenv("ALAYA_VIS_LIMIT")) {  // diagnostics: spill threshold in entries (1 = at the
+      const uint64_t lim = std::strtoull(e, nullptr, 10);  // first expansion); exact up to slots - 64
+      if (lim > 0) p.vis_limit = static_cast<uint32_t>(std::min<uint64_t>(lim, (1ull << l) - 64));
+    }
     return l;
   };
   auto fits_compact = [&](uint32_t l) { return (lbits > l ? lbits - l : 0u) <= kMaxCompactRbits; };
@@ -331,7 +340,7 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   // the register-bound residency, probed with a 4 KB table -- or with the smallest table when a
   // spill table is the second level (a spill then costs a flush and prefetched bucket reads, not a
   // round trip per visit, so residency wins over first-level size)
-  const bool stab = spill_table_log2(p.sq8_order, lbits, ef) != 0;
+  const bool stab = p.stab_log2 != 0;  // set by do_search (spill_table_log2)
   int vgpr_blocks = 0;
   hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + (stab ? 1024 : 4096)), &vgpr_blocks),
             "occupancy");
@@ -408,6 +417,9 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.sq_min = ix->sq_min.as<float>();
     p.sq_max = ix->sq_max.as<float>();
   }
+  // the visited second level: spill table or bitset (decides the kernel for f32 rows too)
+  p.stab_log2 = spill_table_log2(p.sq8_order, std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2))), ef,
+                                 p.generic ? 0u : p.dim);
   // waves per workgroup: never more than the batch needs
   int W = search_waves(p);
   while (W > 1 && static_cast<uint64_t>(W) > nq) W /= 2;

@@ -149,34 +149,48 @@ __device__ __forceinline__ void fold32(float &L, uint32_t &Li, float cd, uint32_
 // full / nonempty: registers whose buffer holds >= kTile / > 0 candidates (uniform).
 // (vector values, not arrays: the fold picks a register by value, which the compiler turns into a
 // dynamic index -- on an array that means scratch memory, on a vector a register move)
-typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
-typedef int i32x16 __attribute__((ext_vector_type(16)));
-struct Shortlists {
-  f32x16 ld, tau;
-  u32x16 li;
-  i32x16 cnt;
+// A consumer may own only part of an accumulator: NR registers starting at register R0 (the
+// two-consumer scan splits the 16 between two waves); register r of the part is accumulator
+// register R0 + r.
+template <int N>
+using f32xN = float __attribute__((ext_vector_type(N)));
+template <int N>
+using u32xN = uint32_t __attribute__((ext_vector_type(N)));
+template <int N>
+using i32xN = int __attribute__((ext_vector_type(N)));
+template <int NR = 16>
+struct ShortlistsT {
+  f32xN<NR> ld, tau;
+  u32xN<NR> li;
+  i32xN<NR> cnt;
   uint32_t full, nonempty;
 };
+using Shortlists = ShortlistsT<16>;
 
-__device__ __forceinline__ void init_shortlists(const FlatParams &p, uint64_t q0, int h, Shortlists &S) {
+// wave-local query of accumulator register r (half h of the wave)
+__device__ __forceinline__ constexpr int reg_query(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <int NR = 16, int R0 = 0>
+__device__ __forceinline__ void init_shortlists(const FlatParams &p, uint64_t q0, int h, ShortlistsT<NR> &S) {
   S.full = S.nonempty = 0;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < NR; ++r) {
     S.ld[r] = FLT_MAX;
     S.li[r] = 0xffffffffu;
-    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const uint64_t qi = q0 + reg_query(R0 + r, h);
     S.tau[r] = (p.tau_init && qi < p.nq) ? p.tau_init[qi] : FLT_MAX;
     S.cnt[r] = 0;
   }
 }
 
 // write the per-(chunk, query) shortlist
-__device__ __forceinline__ void store_shortlists(const FlatParams &p, uint64_t q0, int chunk, const Shortlists &S) {
+template <int NR = 16, int R0 = 0>
+__device__ __forceinline__ void store_shortlists(const FlatParams &p, uint64_t q0, int chunk, const ShortlistsT<NR> &S) {
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const uint64_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+  for (int r = 0; r < NR; ++r) {
+    const uint64_t qi = q0 + reg_query(R0 + r, h);
     if (qi < p.nq) {
       const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
       p.cand_d[o] = S.ld[r];
@@ -188,9 +202,9 @@ __device__ __forceinline__ void store_shortlists(const FlatParams &p, uint64_t q
 // Candidate handling of one 32-row tile: approximate distances a = |b|^2 - 2 c[r] below the
 // query's threshold are appended to its LDS buffer (bd/bi, a stack per query), then the fold
 // rounds that became due run.  last: the wave's final tile (every buffer is drained).
-template <int kB = kBuf>
-__device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x16 &c, float bn, uint32_t rid,
-                                                uint64_t live_mask, bool last, Shortlists &S, float *bd,
+template <int kB = kBuf, int NR = 16, int R0 = 0>
+__device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32xN<NR> &c, float bn, uint32_t rid,
+                                                uint64_t live_mask, bool last, ShortlistsT<NR> &S, float *bd,
                                                 uint32_t *bi, uint64_t &t_app, uint64_t &t_fold) {
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
@@ -201,8 +215,8 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x1
   const uint64_t ta = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
   uint32_t need = 0;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;  // wave-local query of register r, half h
+  for (int r = 0; r < NR; ++r) {
+    const int qloc = reg_query(R0 + r, h);  // wave-local query of register r, half h
     const float dv = fmaf(-2.0f, c[r], bn);
     // the compare's lane mask straight from v_cmp (llvm.amdgcn.fcmp, predicate OLT = 4), no
     // bool round trip through a VGPR
@@ -232,7 +246,7 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x1
   if (need == 0 && S.full) need = 1u << __builtin_ctz(S.full);
   if (p.ablate == 2) {  // diagnostics: appends only, buffers dropped instead of folded
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
+    for (int r = 0; r < NR; ++r)
       if (need & (1u << r)) S.cnt[r] = 0;
     S.full &= ~need;
     S.nonempty &= ~need;
@@ -252,14 +266,14 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x1
       uint32_t Li = S.li[0];
       int cr = S.cnt[0];
 #pragma unroll
-      for (int r2 = 1; r2 < 16; ++r2) {
+      for (int r2 = 1; r2 < NR; ++r2) {
         if (r2 == r) {
           L = S.ld[r2];
           Li = S.li[r2];
           cr = S.cnt[r2];
         }
       }
-      const int qloc = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int qloc = reg_query(R0 + r, h);
       do {  // one round; the last tile repeats until the buffer is empty
         const int start = max(cr - 32, 0);  // uniform per half
         float cd = FLT_MAX;
@@ -276,7 +290,7 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32x1
       if (!__builtin_amdgcn_ballot_w64(cr > 0)) S.nonempty &= ~(1u << r);
       const float th = lane31_of_half(L);
 #pragma unroll
-      for (int r2 = 0; r2 < 16; ++r2) {
+      for (int r2 = 0; r2 < NR; ++r2) {
         if (r2 == r) {
           S.ld[r2] = L;
           S.li[r2] = Li;
@@ -501,8 +515,69 @@ __device__ __forceinline__ void lds_publish(uint32_t *a, uint32_t v) {
   if (__lane_id() == 0) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int K, int kB, int kD>
-__global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
+// The consumer side of flat_scan_ws_kernel: wave `cw` of the pair w handles accumulator registers
+// [R0, R0 + NR) of its producer's tiles -- all 16 with one consumer per producer, 8 each with two.
+template <int kB, int kD, int kCons, int NR, int R0>
+__device__ __forceinline__ void ws_consume(const FlatParams &p, const float *cx, uint32_t *published,
+                                           uint32_t *consumed, uint32_t *abort, float *bd, uint32_t *bi, int w,
+                                           int half, uint64_t q0, int chunk, int ntiles, uint64_t r0, uint64_t r1) {
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  ShortlistsT<NR> S;
+  init_shortlists<NR, R0>(p, q0, h, S);
+  uint64_t t_app = 0, t_fold = 0;
+  __syncthreads();
+  const bool diag = p.merge_count != nullptr;
+  uint64_t t_wait = 0;
+  const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
+  int slot = 0;
+  bool ok = true;
+  const int col = lane & 31;
+  for (int t = 0; t < ntiles; ++t) {
+    const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
+    if (!lds_wait_ge(&published[w], static_cast<uint32_t>(t + 1), abort, p.spin_limit)) {
+      ok = false;
+      break;
+    }
+    if (diag) t_wait += __builtin_amdgcn_s_memtime() - tw;
+    const uint64_t row0 = r0 + static_cast<uint64_t>(kTile) * t;
+    const uint64_t row = row0 + col;
+    const uint32_t rid = static_cast<uint32_t>(row * p.row_step);
+    bool live = row < r1;
+    const float bn = p.norms[(live ? row : r0) * p.row_step];
+    if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
+    const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
+    const float *in = cx + ((slot * 4 + w) * 16 + R0) * 64 + lane;
+    f32xN<NR> c;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) c[r] = in[r * 64];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's reads are done before it is released
+    lds_publish(&consumed[w * kCons + half], static_cast<uint32_t>(t + 1));
+    slot = slot + 1 == kD ? 0 : slot + 1;
+    tile_candidates<kB, NR, R0>(p, c, bn, rid, live_mask, t == ntiles - 1, S, bd, bi, t_app, t_fold);
+  }
+  if (!ok) {
+    // aborted: an unprovable shortlist (cutoff -FLT_MAX, no ids) makes the merge flag every query
+    // of the group, and the flagged queries are recomputed exhaustively
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      S.ld[r] = -FLT_MAX;
+      S.li[r] = 0xffffffffu;
+    }
+  }
+  if (diag && lane == 0) {  // diagnostics: total, appends, fold rounds, waiting for the producer
+    unsigned long long *st =
+        reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * 4 * kCons + w * kCons + half) * 4;
+    st[0] = __builtin_amdgcn_s_memtime() - t_start;
+    st[1] = t_app;
+    st[2] = t_fold;
+    st[3] = t_wait;
+  }
+  store_shortlists<NR, R0>(p, q0, chunk, S);
+}
+
+template <int K, int kB, int kD, int kCons>
+__global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatParams p) {
   static_assert(K % 16 == 0 && K <= 224, "narrow rows");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int kBPitch = K + 8;
@@ -510,10 +585,10 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
   float *tile = reinterpret_cast<float *>(smem);                   // 2 x kTileWords
   float *cx = tile + 2 * kTileWords;                                // kD x 4 waves x 16 regs x 64 lanes
   uint32_t *sync = reinterpret_cast<uint32_t *>(cx + kD * 4 * 16 * 64 + 4 * 32 * kB * 2);
-  uint32_t *published = sync;       // [w]: tiles pair w's producer has written
-  uint32_t *consumed = sync + 4;    // [w]: tiles pair w's consumer has read
-  uint32_t *staged = sync + 8;      // producer arrivals (4 per tile)
-  uint32_t *abort = sync + 9;
+  uint32_t *published = sync;                // [w]: tiles pair w's producer has written
+  uint32_t *consumed = sync + 4;             // [w * kCons + c]: tiles pair w's consumer c has read
+  uint32_t *staged = sync + 4 + 4 * kCons;   // producer arrivals (4 per tile)
+  uint32_t *abort = staged + 1;
   const int wave = threadIdx.x >> 6;
   const int w = wave & 3;
   const int lane = lane_id();
@@ -605,9 +680,15 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c, 0, 0, 0);
       }
-      // ring slot s % kD is free once the consumer has read tile s - kD
+      // ring slot s % kD is free once the consumers have read tile s - kD
       const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-      if (s >= kD && !lds_wait_ge(&consumed[w], static_cast<uint32_t>(s + 1 - kD), abort, p.spin_limit)) break;
+      bool free_slot = true;
+#pragma unroll
+      for (int c2 = 0; c2 < kCons; ++c2)
+        if (s >= kD && free_slot &&
+            !lds_wait_ge(&consumed[w * kCons + c2], static_cast<uint32_t>(s + 1 - kD), abort, p.spin_limit))
+          free_slot = false;
+      if (!free_slot) break;
       if (diag) t_slot += __builtin_amdgcn_s_memtime() - tw;
       float *out = cx + ((slot * 4 + w) * 16) * 64 + lane;
 #pragma unroll
@@ -627,65 +708,25 @@ __global__ void __launch_bounds__(512) flat_scan_ws_kernel(FlatParams p) {
     }
     if (diag && lane == 0) {  // diagnostics: producer rows after the consumers' (tools/flat_diag.py)
       unsigned long long *st =
-          reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (1024 + blockIdx.x * 4 + w) * 4;
+          reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (1024 * kCons + blockIdx.x * 4 + w) * 4;
       st[0] = __builtin_amdgcn_s_memtime() - t_start;
       st[1] = t_slot;
       st[2] = t_staged;
       st[3] = 0;
     }
   } else {
-    // ---- consumer ------------------------------------------------------------------------
-    float *bd = cx + kD * 4 * 16 * 64 + w * 32 * kB * 2;  // 32 queries x kB
+    // ---- consumer(s) ---------------------------------------------------------------------
+    float *bd = cx + kD * 4 * 16 * 64 + w * 32 * kB * 2;  // 32 queries x kB (each consumer its own queries)
     uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
-    Shortlists S;
-    init_shortlists(p, q0, h, S);
-    uint64_t t_app = 0, t_fold = 0;
-    __syncthreads();
-    const bool diag = p.merge_count != nullptr;
-    uint64_t t_wait = 0;
-    const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
-    int slot = 0;
-    bool ok = true;
-    for (int t = 0; t < ntiles; ++t) {
-      const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-      if (!lds_wait_ge(&published[w], static_cast<uint32_t>(t + 1), abort, p.spin_limit)) {
-        ok = false;
-        break;
-      }
-      if (diag) t_wait += __builtin_amdgcn_s_memtime() - tw;
-      const uint64_t row0 = r0 + static_cast<uint64_t>(kTile) * t;
-      const uint64_t row = row0 + col;
-      const uint32_t rid = static_cast<uint32_t>(row * p.row_step);
-      bool live = row < r1;
-      const float bn = p.norms[(live ? row : r0) * p.row_step];
-      if (p.valid != nullptr && live) live = (p.valid[rid >> 5] >> (rid & 31)) & 1u;
-      const uint64_t live_mask = __builtin_amdgcn_ballot_w64(live);
-      const float *in = cx + ((slot * 4 + w) * 16) * 64 + lane;
-      f32x16 c;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) c[r] = in[r * 64];
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's reads are done before it is released
-      lds_publish(&consumed[w], static_cast<uint32_t>(t + 1));
-      slot = slot + 1 == kD ? 0 : slot + 1;
-      tile_candidates<kB>(p, c, bn, rid, live_mask, t == ntiles - 1, S, bd, bi, t_app, t_fold);
+    const int half = (wave - 4) / 4;
+    if constexpr (kCons == 1) {
+      ws_consume<kB, kD, 1, 16, 0>(p, cx, published, consumed, abort, bd, bi, w, 0, q0, chunk, ntiles, r0, r1);
+    } else {
+      if (half == 0)
+        ws_consume<kB, kD, 2, 8, 0>(p, cx, published, consumed, abort, bd, bi, w, 0, q0, chunk, ntiles, r0, r1);
+      else
+        ws_consume<kB, kD, 2, 8, 8>(p, cx, published, consumed, abort, bd, bi, w, 1, q0, chunk, ntiles, r0, r1);
     }
-    if (!ok) {
-      // aborted: an unprovable shortlist (cutoff -FLT_MAX, no ids) makes the merge flag every query
-      // of the group, and the flagged queries are recomputed exhaustively
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        S.ld[r] = -FLT_MAX;
-        S.li[r] = 0xffffffffu;
-      }
-    }
-    if (diag && lane == 0) {  // diagnostics: total, appends, fold rounds, waiting for the producer
-      unsigned long long *st = reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * 4 + w) * 4;
-      st[0] = __builtin_amdgcn_s_memtime() - t_start;
-      st[1] = t_app;
-      st[2] = t_fold;
-      st[3] = t_wait;
-    }
-    store_shortlists(p, q0, chunk, S);
   }
 }
 
@@ -1328,10 +1369,15 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
   // the warp-specialised kernel for the split contraction; the single-role kernel for the f32
   // contraction and the diagnostics (ablation, per-phase stamps)
   const bool ws = p.split && p.ablate == 0 && std::getenv("ALAYA_FLAT_WS0") == nullptr;
+  const char *ws2 = std::getenv("ALAYA_FLAT_WS2");  // two consumers per producer (experiment)
+  const bool two = ws2 && ws2[0] == '1';
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
-    if (ws)                                                                                    \
-      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>()>), dim3(blocks), dim3(512),       \
+    if (ws && two)                                                                             \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>(), 2>), dim3(blocks), dim3(768),    \
+                         ws_lds<K>(), s, p);                                                   \
+    else if (ws)                                                                               \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>(), 1>), dim3(blocks), dim3(512),    \
                          ws_lds<K>(), s, p);                                                   \
     else if (p.split)                                                                          \
       hipLaunchKernelGGL((flat_scan_kernel<K, true>), dim3(blocks), dim3(256), lds, s, p);     \

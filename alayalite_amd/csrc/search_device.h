@@ -542,7 +542,7 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
 template <bool kIP, int kChunks, int kSpace>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out) {
-  if constexpr (kSpace == 0) {
+  if constexpr (kSpace == 0 || kSpace == 3) {  // f32 rows (3: on the spill table)
     row_distances<kIP, kChunks>(p, L.q, ids, n, out);
   } else {
     sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks>(p, L.q, L.sq_scale, L.sq_min, ids, n, out);

@@ -33,15 +33,26 @@
 // the expansion loop (32-136 B of scratch) and keep their natural budget.
 #define ALAYA_MIN_WAVES_SQ8 -1
 #endif
+#ifndef ALAYA_MIN_WAVES_TAB
+#define ALAYA_MIN_WAVES_TAB 5  // d = 128 rows on the spill table: 5 searchers per SIMD (99 -> 96 VGPRs)
+#endif
 #ifndef ALAYA_MIN_WAVES_NARROW
 #define ALAYA_MIN_WAVES_NARROW 0
 #endif
+// kSpace: 0 = f32 rows, 1 = SQ8 codes in the AVX2 order, 2 = SQ8 codes in the AVX-512 order,
+// 3 = f32 rows with the spill table as the visited second level (narrow rows; see spill_table_log2)
+template <int kSpace>
+constexpr bool space_sq8() { return kSpace == 1 || kSpace == 2; }
+template <int kSpace>
+constexpr bool space_tab() { return kSpace == 2 || kSpace == 3; }
+
 template <int kChunks, int kSpace>
 constexpr int search_min_waves() {
-  if constexpr (kSpace != 0) {
+  if constexpr (space_sq8<kSpace>()) {
     if (ALAYA_MIN_WAVES_SQ8 >= 0) return ALAYA_MIN_WAVES_SQ8;
     return kSpace == 2 && kChunks > 0 ? 4 : 0;
   }
+  if constexpr (kSpace == 3) return kChunks <= 4 ? ALAYA_MIN_WAVES_TAB : 0;  // no LDS table: registers bound residency
   return kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : 0;
 }
 
@@ -55,7 +66,7 @@ namespace {
 template <int kSpace>
 __device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *smem, int wave) {
   Lds L;
-  unsigned char *ptr = smem + search_shared_lds_bytes(p.stride, kSpace != 0) + static_cast<size_t>(wave) * p.wave_lds;
+  unsigned char *ptr = smem + search_shared_lds_bytes(p.stride, space_sq8<kSpace>()) + static_cast<size_t>(wave) * p.wave_lds;
   L.q = reinterpret_cast<float *>(ptr);
   ptr += static_cast<size_t>(p.stride) * 4;
   L.cid = reinterpret_cast<uint32_t *>(ptr);
@@ -69,8 +80,8 @@ __device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *s
   L.pi = reinterpret_cast<uint32_t *>(ptr);
   ptr += ((p.ef + 1) * 4 + 15) / 16 * 16;
   L.hash = reinterpret_cast<uint32_t *>(ptr);
-  L.sq_scale = kSpace ? reinterpret_cast<float *>(smem) : nullptr;
-  L.sq_min = kSpace ? reinterpret_cast<float *>(smem) + p.stride : nullptr;
+  L.sq_scale = space_sq8<kSpace>() ? reinterpret_cast<float *>(smem) : nullptr;
+  L.sq_min = space_sq8<kSpace>() ? reinterpret_cast<float *>(smem) + p.stride : nullptr;
   return L;
 }
 
@@ -78,7 +89,7 @@ __device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *s
 // scale = (max - min) * (1/255)), before any wave starts a query.
 template <int kSpace>
 __device__ __forceinline__ void fill_shared(const SearchParams &p, const Lds &L) {
-  if constexpr (kSpace != 0) {
+  if constexpr (space_sq8<kSpace>()) {
     const float kInv255 = 1.0f / 255.0f;
     for (uint32_t e = threadIdx.x; e < p.stride; e += blockDim.x) {
       float sc = 0.f, mn = 0.f;
@@ -103,7 +114,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
   const uint32_t hsize = 1u << p.hash_log2;
   // ---- per-query init ------------------------------------------------------------------
   const float *qsrc = p.queries + static_cast<uint64_t>(qi) * p.q_stride;
-  if constexpr (kSpace == 0) {
+  if constexpr (!space_sq8<kSpace>()) {
     for (uint32_t e = lane; e < p.stride; e += 64) L.q[e] = e < p.dim ? qsrc[e] : 0.f;
   } else {
     // SQ8Space::QueryComputer encodes the query with the quantizer (sq8_space.hpp:266-271,
@@ -138,7 +149,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
   wave_sync();
   vs = make_visited(p, L.hash, slot_bits, slot_dirty, slot_stab);
   ps = PoolState{0u, 0u, p.ef};
-  constexpr bool kTab = kSpace == 2;  // the AVX-512-order SQ8 kernels may run on the spill table
+  constexpr bool kTab = space_tab<kSpace>();  // the kernels that may run on the spill table
 
   // ---- Graph::initialize_search (graph.hpp:148-158) ---------------------------------------
   if (p.levels != nullptr) {
@@ -274,8 +285,9 @@ __global__ void __launch_bounds__(256)
   const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
   uint32_t *slot_bits = p.overflow_bits + slot * bit_words;
   uint32_t *slot_dirty = p.dirty_words + slot * p.dirty_cap;
-  // spill tables only in the SQ8 kernels (a compile-time null elsewhere: the f32 kernels carry none of it)
-  uint16_t *slot_stab = (kSpace == 2 && p.spill_table) ? p.spill_table + (slot << p.stab_log2) : nullptr;
+  // spill tables only in the AVX-512-order SQ8 kernels and the kSpace = 3 f32 kernels (a
+  // compile-time null elsewhere: the default f32 kernels carry none of it)
+  uint16_t *slot_stab = (space_tab<kSpace>() && p.spill_table) ? p.spill_table + (slot << p.stab_log2) : nullptr;
 
   for (;;) {
     uint32_t qi = 0;
@@ -340,8 +352,8 @@ __global__ void __launch_bounds__(256)
           if (j < lane && vj == v) act = false;
         }
       }
-      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin<kSpace == 2>(vs);
-      const bool fresh = visit<kSpace == 2>(vs, v, act, kSpillPrefetch && u == pre_u, pre_lo, pre_hi);
+      if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin<space_tab<kSpace>()>(vs);
+      const bool fresh = visit<space_tab<kSpace>()>(vs, v, act, kSpillPrefetch && u == pre_u, pre_lo, pre_hi);
       // consumed: the prefetched state describes the table only up to this visit's stores, so it
       // is never reused (an expansion without fresh neighbours skips the prefetch below, and the
       // next pop must not take this one for its own); zeroed so it is not live across the
@@ -570,10 +582,14 @@ static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped) {
   return ip ? kernel_ptr<true, 0, false, kSpace>() : kernel_ptr<false, 0, false, kSpace>();
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic) {
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic, bool tab) {
   if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped);
   if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped);
   const uint32_t chunks = (!generic && dim % 32 == 0) ? dim / 32 : 0;  // generic order: the runtime-d kernel
+  if (tab && !stamped) {  // f32 rows on the spill table (spill_table_log2 enables it for these shapes)
+    if (chunks == 4) return ip ? kernel_ptr<true, 4, false, 3>() : kernel_ptr<false, 4, false, 3>();
+    if (chunks == 8) return ip ? kernel_ptr<true, 8, false, 3>() : kernel_ptr<false, 8, false, 3>();
+  }
   if (stamped) {
     if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();
     if (chunks == 4) return ip ? kernel_ptr<true, 4, true>() : kernel_ptr<false, 4, true>();
@@ -592,7 +608,7 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_or
 }
 
 hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic, p.stab_log2 != 0);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64 * waves), args, lds, stream);
@@ -611,7 +627,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 }
 
 hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic, p.stab_log2 != 0);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * waves, lds);
 }
 

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--table", default="0", help="slots per ef targets (0 = default policy); negative = fixed log2")
     ap.add_argument("--spill-table", default="d",
                     help="ALAYA_SPILL_TABLE values: d = the engine's default, 0 = bitset second level, 6..16 = log2 entries")
+    ap.add_argument("--env-sweep", default="", help="NAME=v1,v2,...: also sweep an environment knob ('-' = unset)")
+    ap.add_argument("--envs", default="", help="environment variants: comma-separated, each '-' (none) or "
+                                               "NAME=VAL+NAME=VAL...; applied on top of --env-sweep")
     ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     import torch
@@ -63,8 +66,23 @@ def main():
         ids = torch.empty((nq, 10), dtype=torch.int32, device="cuda")
         dd = torch.empty((nq, 10), dtype=torch.float32, device="cuda")
         cnt = torch.empty((nq, 4), dtype=torch.int32, device="cuda")
-        for w, mw, vm, stb in [(w, mw, vm, stb) for w in args.waves.split(",") for mw in args.max_waves.split(",")
-                               for vm in args.visited.split(",") for stb in args.spill_table.split(",")]:
+        env_name, env_vals = (args.env_sweep.split("=", 1)[0], args.env_sweep.split("=", 1)[1].split(",")) \
+            if args.env_sweep else ("", ["-"])
+        variants = args.envs.split(",") if args.envs else ["-"]
+        known = {kv.split("=", 1)[0] for v_ in variants if v_ != "-" for kv in v_.split("+")}
+        for w, mw, vm, stb, ev, var in [(w, mw, vm, stb, ev, var) for w in args.waves.split(",")
+                                        for mw in args.max_waves.split(",") for vm in args.visited.split(",")
+                                        for stb in args.spill_table.split(",") for ev in env_vals for var in variants]:
+            if env_name:
+                os.environ.pop(env_name, None)
+                if ev != "-":
+                    os.environ[env_name] = ev
+            for k in known:
+                os.environ.pop(k, None)
+            if var != "-":
+                for kv in var.split("+"):
+                    k, v_ = kv.split("=", 1)
+                    os.environ[k] = v_
             os.environ.pop("ALAYA_SPILL_TABLE", None)
             if stb != "d":
                 os.environ["ALAYA_SPILL_TABLE"] = stb
@@ -102,7 +120,8 @@ def main():
                 ms = e0.elapsed_time(e1) / args.reps
                 h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
                 c = cnt.cpu().numpy()
-                print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb} spill-table {stb}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
+                print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb} spill-table {stb}"
+                      f"{f' {env_name}={ev}' if env_name else ''}{f' [{var}]' if var != '-' else ''}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
                       f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}", flush=True)
     os.environ.pop("ALAYA_SEARCH_WAVES", None)
     os.environ.pop("ALAYA_MAX_WAVES_PER_CU", None)
