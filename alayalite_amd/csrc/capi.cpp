@@ -335,6 +335,13 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     if (compact && !fits_compact(l)) throw ArgError("compact visited table cannot encode ids of this index");
     return set_mode(l, compact);
   }
+  if (p.stab_log2 != 0 && mode != 1 && mode != 3) {
+    // The spill table is the second level: a query spills at its first expansion into a 128-slot
+    // first level, then every visit is prefetched bucket reads (config 5: 10k queries 9.30 ->
+    // 9.20 ms, 1k queries 3.89 -> 3.69 ms against first levels sized for LDS;
+    // profiles/r04/spill_table/c5_first_level_size_threshold.log).  LDS then bounds nothing.
+    return set_mode(7, false);
+  }
   const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0);
   const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
   // the register-bound residency, probed with a 4 KB table -- or with the smallest table when a

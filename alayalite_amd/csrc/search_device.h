@@ -76,6 +76,9 @@ struct Lds {
 template <bool kIP, int kChunks, int kSpace>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out);
+template <bool kIP, int kChunks, int kSpace, typename Hook>
+__device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
+                                                const uint32_t *ids, int n, float *out, Hook after_issue);
 
 template <bool kIP>
 __device__ __forceinline__ void accumulate(const float4 x, const float4 y, float &a0, float &a1,
@@ -455,10 +458,16 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
   }
 }
 
-template <bool kIP, int kOrder, int kFull>
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+// after_issue() runs once, right after the first pass's row loads are issued (the search kernel
+// issues its second-level prefetch there, so it overlaps the rows' latency)
+template <bool kIP, int kOrder, int kFull, typename Hook = NoHook>
 __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float *xq,
                                               const float *sc, const float *mnv,
-                                              const uint32_t *ids, int n, float *out) {
+                                              const uint32_t *ids, int n, float *out, Hook after_issue = Hook()) {
   constexpr int P = kOrder == 2 ? 32 : 16;
   constexpr int LPR = P / 4;    // lanes per row
   constexpr int G = 64 / LPR;   // row groups per wave
@@ -467,11 +476,13 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
     for (int base = 0; base < n; base += G * kRPL) {
       Sq8Pass<kOrder, kFull> S;
       sq8_issue<kOrder, kFull>(p, ids, n, base, S);
+      if (base == 0) after_issue();
       sq8_finish<kIP, kOrder, kFull>(p, xq, sc, mnv, n, base, S, out);
     }
     wave_sync();
     return;
   }
+  after_issue();
   const int lane = lane_id();
   const int g = lane / LPR, m = lane % LPR;
   const int T = kFull > 0 ? kFull : static_cast<int>(p.dim) / P;
@@ -539,14 +550,22 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
   wave_sync();
 }
 
+template <bool kIP, int kChunks, int kSpace, typename Hook>
+__device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
+                                                const uint32_t *ids, int n, float *out, Hook after_issue) {
+  if constexpr (kSpace == 0 || kSpace == 3) {  // f32 rows (3: on the spill table)
+    row_distances<kIP, kChunks>(p, L.q, ids, n, out);
+    after_issue();
+  } else {
+    sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks>(p, L.q, L.sq_scale, L.sq_min, ids, n, out,
+                                                                      after_issue);
+  }
+}
+
 template <bool kIP, int kChunks, int kSpace>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out) {
-  if constexpr (kSpace == 0 || kSpace == 3) {  // f32 rows (3: on the spill table)
-    row_distances<kIP, kChunks>(p, L.q, ids, n, out);
-  } else {
-    sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks>(p, L.q, L.sq_scale, L.sq_min, ids, n, out);
-  }
+  space_distances<kIP, kChunks, kSpace>(p, L, ids, n, out, NoHook());
 }
 
 // --------------------------------------------------------------------------------------------

@@ -376,14 +376,20 @@ __global__ void __launch_bounds__(256)
       const uint32_t slot = __popcll(fm & ((1ull << lane) - 1ull));
       if (fresh) L.cid[slot] = v;
       wave_sync();
-      space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd);
-      if constexpr (kSpillPrefetch) {
-        if (vs.spilled && pred != kEmpty && !(p.spill_flags & 1u)) {
-          __builtin_amdgcn_s_waitcnt(0);  // this expansion's second-level stores / atomics have landed in L2
-          spill_prefetch(vs, pred_v, lane < static_cast<int>(p.R), pre_lo, pre_hi);
-          pre_u = pred;
+      // The second-level prefetch of the predicted next expansion goes out right after this
+      // expansion's first row pass is issued, so its latency overlaps the rows'.  It needs pred_v,
+      // which was loaded after this visit's stores and atomics and before the rows: the wait for
+      // pred_v (vmcnt counts loads, stores and atomics in issue order) is the wait for them too, so
+      // the prefetch reads the table as this visit left it.
+      space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd, [&]() {
+        if constexpr (kSpillPrefetch) {
+          if (vs.spilled && pred != kEmpty && !(p.spill_flags & 1u)) {
+            if (p.spill_flags & 4u) __builtin_amdgcn_s_waitcnt(0);  // diagnostics: also wait for the rows
+            spill_prefetch(vs, pred_v, lane < static_cast<int>(p.R), pre_lo, pre_hi);
+            pre_u = pred;
+          }
         }
-      }
+      });
       stamp(3);
       n_dist += nf;
       const bool has = lane < nf;

@@ -69,8 +69,9 @@ def _run(native, setup, order, metric, ef, visited_mode=0, log2_slots=7):
             assert tuple(s_c[i]) == tuple(o_c), (rep, i, s_c[i], o_c)
             assert np.array_equal(r_ids[i], rr[i][0]), (rep, i, r_ids[i], rr[i][0])
             assert np.array_equal(r_d[i].view(np.uint32), rr[i][1].view(np.uint32)), (rep, i)
-        # far past the ids the first level holds before it spills
-        assert s_c[:, 0].min() > 150, s_c[:, 0].min()
+        # far past the ids the first level holds before it spills (~25 with 128 slots; the
+        # multi-threaded host build varies the graph, so the margin is generous)
+        assert s_c[:, 0].min() > 100, s_c[:, 0].min()
 
 
 @pytest.mark.parametrize("ef", [40, 340])
