@@ -211,16 +211,11 @@ constexpr uint32_t kDirtyCap = 16384;  // per-slot dirty-word list (64 KB): word
 // hash's low L - (s - 3) bits) fits 16 bits; at most 2^16 (128 KB per slot; ids wider than 28 bits
 // keep the bitset).  ALAYA_SPILL_TABLE=0 keeps the bitset, a value 6..16 forces the size (tests: tiny
 // tables fill their buckets and exercise the bitset fallback).
-uint32_t spill_table_log2(int sq8_order, uint32_t L, uint32_t ef, uint32_t dim = 0) {
-  // The AVX2-order SQ8 kernels (hosts without AVX-512) keep the bitset: the table's state would
-  // overrun their SGPR budget (65-116 restores per expansion).  f32 kernels: their tables rarely
-  // spill, they keep the bitset unless ALAYA_SPILL_TABLE_F32=1 (narrow rows, dim <= 256 in 32s:
-  // an experiment with the LDS first level bypassed)
-  if (sq8_order == 1) return 0;
-  if (sq8_order == 0) {
-    const char *f = std::getenv("ALAYA_SPILL_TABLE_F32");
-    if (!(f && f[0] == '1') || dim == 0 || dim > 256 || dim % 32 != 0) return 0;
-  }
+uint32_t spill_table_log2(int sq8_order, uint32_t L, uint32_t ef) {
+  // f32 kernels keep the LDS first level and the bitset (their tables rarely spill; on the spill
+  // table SIFT ran 23 % slower); so do the AVX2-order SQ8 kernels (hosts without AVX-512), whose
+  // SGPR budget the table's state would overrun (65-116 restores per expansion)
+  if (sq8_order != 2) return 0;
   uint32_t s = std::max<uint32_t>({6u, ceil_log2(32ull * ef), L > 12 ? L - 12 : 0u});
   if (const char *e = std::getenv("ALAYA_SPILL_TABLE")) {
     const uint32_t v = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
@@ -424,9 +419,8 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.sq_min = ix->sq_min.as<float>();
     p.sq_max = ix->sq_max.as<float>();
   }
-  // the visited second level: spill table or bitset (decides the kernel for f32 rows too)
-  p.stab_log2 = spill_table_log2(p.sq8_order, std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2))), ef,
-                                 p.generic ? 0u : p.dim);
+  // the visited second level: spill table or bitset
+  p.stab_log2 = spill_table_log2(p.sq8_order, std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2))), ef);
   // waves per workgroup: never more than the batch needs
   int W = search_waves(p);
   while (W > 1 && static_cast<uint64_t>(W) > nq) W /= 2;

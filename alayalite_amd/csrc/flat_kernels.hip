@@ -1369,8 +1369,10 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
   // the warp-specialised kernel for the split contraction; the single-role kernel for the f32
   // contraction and the diagnostics (ablation, per-phase stamps)
   const bool ws = p.split && p.ablate == 0 && std::getenv("ALAYA_FLAT_WS0") == nullptr;
-  const char *ws2 = std::getenv("ALAYA_FLAT_WS2");  // two consumers per producer (experiment)
-  const bool two = ws2 && ws2[0] == '1';
+  // two consumer waves per producer (default): config 2 566k -> 617k QPS (scan 1.76 -> 1.61 ms,
+  // profiles/r04/flat/); ALAYA_FLAT_WS2=0 keeps one
+  const char *ws2 = std::getenv("ALAYA_FLAT_WS2");
+  const bool two = !(ws2 && ws2[0] == '0');
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
     if (ws && two)                                                                             \

@@ -553,7 +553,7 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
 template <bool kIP, int kChunks, int kSpace, typename Hook>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out, Hook after_issue) {
-  if constexpr (kSpace == 0 || kSpace == 3) {  // f32 rows (3: on the spill table)
+  if constexpr (kSpace == 0) {
     row_distances<kIP, kChunks>(p, L.q, ids, n, out);
     after_issue();
   } else {

@@ -33,18 +33,17 @@
 // the expansion loop (32-136 B of scratch) and keep their natural budget.
 #define ALAYA_MIN_WAVES_SQ8 -1
 #endif
-#ifndef ALAYA_MIN_WAVES_TAB
-#define ALAYA_MIN_WAVES_TAB 5  // d = 128 rows on the spill table: 5 searchers per SIMD (99 -> 96 VGPRs)
-#endif
 #ifndef ALAYA_MIN_WAVES_NARROW
 #define ALAYA_MIN_WAVES_NARROW 0
 #endif
-// kSpace: 0 = f32 rows, 1 = SQ8 codes in the AVX2 order, 2 = SQ8 codes in the AVX-512 order,
-// 3 = f32 rows with the spill table as the visited second level (narrow rows; see spill_table_log2)
+// kSpace: 0 = f32 rows, 1 = SQ8 codes in the AVX2 order, 2 = SQ8 codes in the AVX-512 order (the
+// kernels that run on the spill table).  f32 rows on the spill table were measured and dropped:
+// SIFT 1M at 10k queries 1.19 -> 1.47 ms, at 1k 0.55 -> 0.68 ms
+// (profiles/r04/search_experiments/sift_spill_table_rejected.log).
 template <int kSpace>
 constexpr bool space_sq8() { return kSpace == 1 || kSpace == 2; }
 template <int kSpace>
-constexpr bool space_tab() { return kSpace == 2 || kSpace == 3; }
+constexpr bool space_tab() { return kSpace == 2; }
 
 template <int kChunks, int kSpace>
 constexpr int search_min_waves() {
@@ -52,7 +51,6 @@ constexpr int search_min_waves() {
     if (ALAYA_MIN_WAVES_SQ8 >= 0) return ALAYA_MIN_WAVES_SQ8;
     return kSpace == 2 && kChunks > 0 ? 4 : 0;
   }
-  if constexpr (kSpace == 3) return kChunks <= 4 ? ALAYA_MIN_WAVES_TAB : 0;  // no LDS table: registers bound residency
   return kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : 0;
 }
 
@@ -285,8 +283,8 @@ __global__ void __launch_bounds__(256)
   const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
   uint32_t *slot_bits = p.overflow_bits + slot * bit_words;
   uint32_t *slot_dirty = p.dirty_words + slot * p.dirty_cap;
-  // spill tables only in the AVX-512-order SQ8 kernels and the kSpace = 3 f32 kernels (a
-  // compile-time null elsewhere: the default f32 kernels carry none of it)
+  // spill tables only in the AVX-512-order SQ8 kernels (a compile-time null elsewhere: the f32
+  // kernels carry none of it)
   uint16_t *slot_stab = (space_tab<kSpace>() && p.spill_table) ? p.spill_table + (slot << p.stab_log2) : nullptr;
 
   for (;;) {
@@ -588,14 +586,10 @@ static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped) {
   return ip ? kernel_ptr<true, 0, false, kSpace>() : kernel_ptr<false, 0, false, kSpace>();
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic, bool tab) {
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic) {
   if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped);
   if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped);
   const uint32_t chunks = (!generic && dim % 32 == 0) ? dim / 32 : 0;  // generic order: the runtime-d kernel
-  if (tab && !stamped) {  // f32 rows on the spill table (spill_table_log2 enables it for these shapes)
-    if (chunks == 4) return ip ? kernel_ptr<true, 4, false, 3>() : kernel_ptr<false, 4, false, 3>();
-    if (chunks == 8) return ip ? kernel_ptr<true, 8, false, 3>() : kernel_ptr<false, 8, false, 3>();
-  }
   if (stamped) {
     if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();
     if (chunks == 4) return ip ? kernel_ptr<true, 4, true>() : kernel_ptr<false, 4, true>();
@@ -614,7 +608,7 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_or
 }
 
 hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic, p.stab_log2 != 0);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64 * waves), args, lds, stream);
@@ -633,7 +627,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 }
 
 hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic, p.stab_log2 != 0);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * waves, lds);
 }
 

@@ -8,18 +8,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["split", "f32", "split-prescan2", "f32-prescan3", "split-ws2"], autouse=True)
+@pytest.fixture(params=["split", "f32", "split-prescan2", "f32-prescan3", "split-ws1"], autouse=True)
 def flat_mode(request, monkeypatch):
     """Both shortlist contractions: the bf16 hi/lo split (default) and the f32 MFMA
     (ALAYA_FLAT_F32).  The exact rescoring and the bound check make the answer identical.
     The prescan (a scan over every S-th row that seeds each chunk's threshold; off by default,
-    ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes; split-ws2 runs the warp-specialised
-    scan with two consumer waves per producer (ALAYA_FLAT_WS2=1)."""
+    ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes.  The warp-specialised scan runs two
+    consumer waves per producer by default; split-ws1 forces one (ALAYA_FLAT_WS2=0)."""
     monkeypatch.delenv("ALAYA_FLAT_F32", raising=False)
     monkeypatch.delenv("ALAYA_FLAT_PRESCAN", raising=False)
     monkeypatch.delenv("ALAYA_FLAT_WS2", raising=False)
-    if request.param == "split-ws2":
-        monkeypatch.setenv("ALAYA_FLAT_WS2", "1")
+    if request.param == "split-ws1":
+        monkeypatch.setenv("ALAYA_FLAT_WS2", "0")
     if request.param.startswith("f32"):
         monkeypatch.setenv("ALAYA_FLAT_F32", "1")
     if "prescan" in request.param:
@@ -130,14 +130,14 @@ def test_flat_ties_and_fallback(native, orc):
 def test_flat_spin_abort_is_flagged_and_redone(native, orc, flat_mode, monkeypatch):
     """The warp-specialised scan gives up on an LDS flag after ALAYA_FLAT_SPIN_LIMIT polls: its
     consumers then write unprovable shortlists.  Forced with a zero limit, the device entry flags
-    every query of an aborted consumer (aligned blocks of 32 queries, or 16 with two consumers per
-    producer, all or none), and flat_search's
+    every query of an aborted consumer (aligned blocks of 16 queries with two consumers per producer,
+    32 with one, all or none), and flat_search's
     exhaustive redo still returns the exact answer."""
     import torch
 
-    if flat_mode not in ("split", "split-ws2"):
+    if flat_mode not in ("split", "split-ws1"):
         pytest.skip("the ring protocol belongs to the split (warp-specialised) scan")
-    group = 16 if flat_mode == "split-ws2" else 32  # queries per consumer wave
+    group = 32 if flat_mode == "split-ws1" else 16  # queries per consumer wave
     monkeypatch.setenv("ALAYA_FLAT_SPIN_LIMIT", "0")
     rng = np.random.default_rng(44)
     base = np.ascontiguousarray(rng.random((20000, 128), dtype=np.float32))

@@ -57,13 +57,14 @@ def test_sq8_expansion_loops_restore_few_spilled_sgpr(census, space, chunks):
 
 def test_register_budgets(census):
     # no scratch traffic per expansion in any search kernel, and no scratch at all outside the
-    # AVX-512-order SQ8 kernels and the f32 spill-table kernels -- those are held to 128 / 96 VGPRs
-    # (4 / 5 waves per SIMD; config 5's 768-d IP kernel needs 129), which costs one 8-byte value
-    # live across the query loop: one store at kernel entry, one load after the loop.  The d = 128 kernels stay at >= 4 waves per SIMD (the
+    # AVX-512-order SQ8 kernels -- those are held to 128 VGPRs (4 waves per SIMD; config 5's 768-d IP
+    # kernel needs 129), which costs a value or two live across the query loop: stored at kernel
+    # entry, loaded after the loop.  The d = 128 kernels stay at >= 4 waves per SIMD (the
     # residency cap is 4).
     for k, r in census.items():
-        assert r["scratch_ops_in_expansion_loops"] == 0, k
-        if ("sq8-avx512" in k or "f32-table" in k) and "chunks=0" not in k and "stamp=0" in k:
+        if "stamp=0" in k:  # (the stamped kernels are diagnostics builds)
+            assert r["scratch_ops_in_expansion_loops"] == 0, k
+        if "sq8-avx512" in k and "chunks=0" not in k and "stamp=0" in k:
             assert r.get("ScratchSize", 0) <= 32 and r["scratch_ops_total"] <= 8, (k, r.get("ScratchSize"))
         elif "stamp=0" in k:
             assert r.get("ScratchSize", 0) == 0, k

@@ -128,31 +128,3 @@ def test_spill_threshold_keeps_results_exact(native, orc, monkeypatch, mode, pct
     dev.set_visited_mode(mode)
     _check(view, *dev.search(queries, 10, 150), queries, 10, 150)
 
-
-@pytest.mark.parametrize("vis_limit", [None, "1"])
-@pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("d", [128, 256])
-def test_f32_rows_on_the_spill_table(native, orc, monkeypatch, vis_limit, metric, d):
-    """The narrow f32 kernels on the spill table (kSpace = 3, ALAYA_SPILL_TABLE_F32=1): the first
-    level spills into the table (or is bypassed from the first expansion, ALAYA_VIS_LIMIT=1), the
-    buckets are read one expansion ahead; 400 queries over few slots, twice, including a table so
-    small (ALAYA_SPILL_TABLE=7) that buckets fill and ids take the bitset third level."""
-    monkeypatch.setenv("ALAYA_SPILL_TABLE_F32", "1")
-    if vis_limit:
-        monkeypatch.setenv("ALAYA_VIS_LIMIT", vis_limit)
-    rng = np.random.default_rng(50 + d + metric)
-    base = rng.standard_normal((12000, d)).astype(np.float32)
-    queries = rng.standard_normal((400, d)).astype(np.float32)
-    g = native.Graph.build(base, metric, 32, 100, 8, 100)
-    l0, levels, off, ue, ep, upper_r, _ = g.arrays()
-    view = orc.IndexView(base, l0, levels, off, ue, upper_r, ep, metric=metric)
-    for table in (None, "7"):
-        if table:
-            monkeypatch.setenv("ALAYA_SPILL_TABLE", table)
-        dev = native.DeviceIndex(0)
-        dev.set_base(base, metric)
-        dev.set_graph(g)
-        dev.set_hash_log2(7)
-        for rep in range(2):
-            qs = queries if rep == 0 else queries[::-1].copy()
-            _check(view, *dev.search(qs, 10, 80), qs, 10, 80)

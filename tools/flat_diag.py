@@ -28,10 +28,11 @@ for ablate in (0, 1, 2, 0, 1, 2):
     b.record()
     torch.cuda.synchronize()
     m = mc.cpu().numpy()
-    sm = mc[4096:].cpu().numpy().view(np.uint64).reshape(-1, 4)[:1024].astype(np.float64)
+    kc = 1 if os.environ.get("ALAYA_FLAT_WS2") == "0" else 2  # consumer waves per producer
+    sm = mc[4096:].cpu().numpy().view(np.uint64).reshape(-1, 4)[:1024 * kc].astype(np.float64)
     st = sm; tot = st[:, 0].mean()
     print(f"   per-wave memtime ticks: total {tot:.0f} append {st[:,1].mean()/tot:.2f} fold {st[:,2].mean()/tot:.2f} (max-wave {st[:,2].max()/tot:.2f}) barrier/wait {st[:,3].mean()/tot:.2f}")
-    pr = mc[4096:].cpu().numpy().view(np.uint64).reshape(-1, 4)[1024:2048].astype(np.float64)
+    pr = mc[4096:].cpu().numpy().view(np.uint64).reshape(-1, 4)[1024 * kc:1024 * kc + 1024].astype(np.float64)
     if ablate == 0 and pr[:, 0].mean() > 0:  # warp-specialised scan: producer rows
         pt = pr[:, 0].mean()
         print(f"   producers: total {pt:.0f} wait-for-slot {pr[:,1].mean()/pt:.2f} wait-for-staging {pr[:,2].mean()/pt:.2f}")

@@ -42,7 +42,7 @@ def demangle(name: str) -> str:
     if not m:
         return name
     ip, chunks, stamp, space = m.groups()
-    return f"{'ip' if ip == '1' else 'l2'} chunks={chunks} stamp={stamp} space={['f32', 'sq8-avx2', 'sq8-avx512', 'f32-table'][int(space)]}"
+    return f"{'ip' if ip == '1' else 'l2'} chunks={chunks} stamp={stamp} space={['f32', 'sq8-avx2', 'sq8-avx512'][int(space)]}"
 
 
 def split_functions(asm: str) -> dict[str, list[str]]:
