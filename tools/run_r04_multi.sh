@@ -7,5 +7,5 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 source tools/gpu_steps.sh
-step 900 gpurun_out/r04_rehearsal_c4.log python -u tools/shard_rehearsal.py --workload gist --nq 10000 --out gpurun_out/shard_rehearsal_c4_10k.json
-step 1000 gpurun_out/r04_rehearsal_c5.log python -u tools/shard_rehearsal.py --workload sq8 --nq 10000 --out gpurun_out/shard_rehearsal_c5_10k.json
+step 450 gpurun_out/r04_rehearsal_c4.log python -u tools/shard_rehearsal.py --workload gist --nq 10000 --out gpurun_out/shard_rehearsal_c4_10k.json
+step 700 gpurun_out/r04_rehearsal_c5.log python -u tools/shard_rehearsal.py --workload sq8 --nq 10000 --out gpurun_out/shard_rehearsal_c5_10k.json
