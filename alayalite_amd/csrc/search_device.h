@@ -988,7 +988,7 @@ struct NoMark {
   __device__ void operator()() const {}
 };
 
-template <typename OnNext = NoNext, typename Mark = NoMark>
+template <bool kRegMerge = false, typename OnNext = NoNext, typename Mark = NoMark>
 __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d,
                            OnNext on_next = OnNext(), Mark mark = Mark()) {
   const int lane = lane_id();
@@ -998,6 +998,58 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   const uint64_t amask = ballot(acc);
   const uint32_t n_acc = __popcll(amask);
   if (n_acc == 0) return;
+  if (kRegMerge && ps.ef <= 128) {
+    // Pools of up to 128 entries (ef <= 128: SIFT-shaped searches) merge from registers: lane l
+    // holds entries l and 64 + l, and one pass over the accepted lanes yields every candidate's
+    // rank, its upper bound in the pool (a ballot count, == the binary search on a sorted pool)
+    // and every entry's shift (#accepted strictly below it, == batch_lower_bound) -- no dependent
+    // LDS round trips.  A NaN anywhere (pool or batch) takes the binary-search path below, whose
+    // answers on such input are the oracle's.
+    const uint32_t size = ps.size;
+    const bool v0 = static_cast<uint32_t>(lane) < size;
+    const bool v1 = static_cast<uint32_t>(lane) + 64 < size;
+    const float p0 = v0 ? L.pd[lane] : 0.f;
+    const float p1 = v1 ? L.pd[lane + 64] : 0.f;
+    const uint32_t i0 = v0 ? L.pi[lane] : 0u;
+    const uint32_t i1 = v1 ? L.pi[lane + 64] : 0u;
+    if (!ballot((acc && d != d) || (v0 && p0 != p0) || (v1 && p1 != p1))) {
+      uint32_t rank = 0, pos = 0, s0 = 0, s1 = 0;
+      uint64_t rest = amask;
+      while (rest) {
+        const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
+        rest &= rest - 1;
+        const float dj = read_lane(d, j);
+        rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
+        const uint32_t ub = __popcll(ballot(v0 && p0 <= dj)) + __popcll(ballot(v1 && p1 <= dj));
+        if (lane == j) pos = ub;
+        s0 += dj < p0 ? 1u : 0u;
+        s1 += dj < p1 ? 1u : 0u;
+      }
+      pos += rank;
+      const int lane0 = __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1;
+      const uint32_t first_pos = read_lane(pos, lane0);
+      if (first_pos <= ps.cur) on_next(read_lane(id, lane0));
+      mark();
+      wave_sync();
+      // an entry with a nonzero shift sits at or after first_pos; destinations are distinct
+      if (v0 && s0 != 0 && lane + s0 < ps.ef) {
+        L.pd[lane + s0] = p0;
+        L.pi[lane + s0] = i0;
+      }
+      if (v1 && s1 != 0 && lane + 64 + s1 < ps.ef) {
+        L.pd[lane + 64 + s1] = p1;
+        L.pi[lane + 64 + s1] = i1;
+      }
+      if (acc && pos < ps.ef) {
+        L.pd[pos] = d;
+        L.pi[pos] = id;
+      }
+      wave_sync();
+      ps.size = min(size + n_acc, ps.ef);
+      if (first_pos < ps.cur) ps.cur = first_pos;
+      return;
+    }
+  }
   // stable rank of this candidate among accepted ones, ordered by (dist, arrival)
   uint32_t rank = 0;
   uint64_t rest = amask;

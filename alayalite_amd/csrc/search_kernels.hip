@@ -320,6 +320,10 @@ __global__ void __launch_bounds__(256)
     // residency): 10.43 -> 9.76 ms with the bitset.  The f32 shapes rarely spill at their table
     // sizes and measured 0.8 % slower with it (profiles/r03/search_experiments/).
     constexpr bool kSpillPrefetch = kSpace != 0;
+    // Register merge (pool_merge, pools of <= 128 entries) in the small-row f32 kernels, whose ef
+    // at recall 0.95 is ~70 (SIFT-shaped); the SQ8 / wide-row kernels run ef ~370 and keep their
+    // registers for the row pass.
+    constexpr bool kRegMerge = kSpace == 0 && kChunks > 0 && kChunks <= 8;
     uint32_t pre_u = kEmpty;
     uint64_t pre_lo = 0ull, pre_hi = 0ull;
     while (ps.cur < ps.size) {
@@ -396,7 +400,7 @@ __global__ void __launch_bounds__(256)
       wave_sync();
       // the merge reports the next pop when it is a newcomer: load its adjacency row while the
       // rest of the merge and the pop run (the prediction above is then stale)
-      pool_merge(ps, L, has, cid, cd, [&](uint32_t nx) {
+      pool_merge<kRegMerge>(ps, L, has, cid, cd, [&](uint32_t nx) {
         if (nx != pred) {
           pred = nx;
           if (lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(nx) * p.R + lane];

@@ -63,6 +63,20 @@ def test_search_k_ef_shapes(native, orc, c1, k, ef):
     _check(view, _dev(native, base, g), queries, k, ef)
 
 
+@pytest.mark.parametrize("dim", [64, 128, 256])
+@pytest.mark.parametrize("ef", [16, 64, 70, 127, 128, 129, 200])
+def test_search_ties_pool_merge(native, orc, dim, ef):
+    """Small-integer rows tie on most distances: the pool's (distance, arrival) order is all that
+    separates them.  ef <= 128 runs the small-row kernels' register merge, ef > 128 the
+    binary-search merge; both must match LinearPool::insert's order (the oracle)."""
+    rng = np.random.default_rng(dim + ef)
+    base = rng.integers(0, 3, (3000, dim)).astype(np.float32)
+    queries = rng.integers(0, 3, (24, dim)).astype(np.float32)
+    queries[:4] = base[:4]  # exact hits: distance 0 ties among duplicates
+    g, view = _graph_view(native, orc, base)
+    _check(view, _dev(native, base, g), queries, 10, ef)
+
+
 def test_k_larger_than_ef(native, orc, c1):
     """k > ef reads past LinearPool's live entries in the reference (slot ef holds the last dropped
     neighbour, beyond it is out of bounds: query_utils.hpp:238, graph_search_job.hpp:254-256).
