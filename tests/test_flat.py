@@ -173,6 +173,33 @@ def test_flat_duplicates_sift_like(native, orc):
     assert np.array_equal(ids, ref_i) and np.array_equal(dists, ref_d)
 
 
+@pytest.fixture(scope="module")
+def flat_1m(orc):
+    """Config 2's shape at full size: 1M x 128 rows, 256 queries (8 query groups); the oracle's
+    find_exact_gt restatement on 16 threads (continuous data: no ties to order)."""
+    rng = np.random.default_rng(1_000_000)
+    base = rng.random((1_000_000, 128), dtype=np.float32)
+    q = rng.random((256, 128), dtype=np.float32)
+    ref_i, _ = orc.exact_gt(base, q, 10, num_threads=16)
+    return base, q, ref_i.astype(np.uint32)
+
+
+def test_flat_exact_1m(native, orc, flat_1m):
+    """Every chunk of a 1M-row scan and the hand-over ring at config 2's chunk count: ids equal the
+    oracle's, and each returned distance is the oracle's distance of that row, bit for bit."""
+    base, q, ref_i = flat_1m
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    assert np.array_equal(ids, ref_i)
+    lib = orc.lib()
+    for a in (0, 77, 255):
+        qa = np.ascontiguousarray(q[a])
+        ref_d = np.array([lib.orc_l2_f32(orc._ptr(qa), orc._ptr(base[i]), 128) for i in ids[a]], np.float32)
+        assert np.array_equal(dists[a].view(np.uint32), ref_d.view(np.uint32))
+    assert redo == 0
+
+
 def test_calc_gt_device_matches_calc_gt(native):
     """The public device helper (the flat path behind alayalite_amd.calc_gt_device) agrees with the
     reference's float64 calc_gt (python/src/alayalite/utils.py:99-105) on continuous data."""
