@@ -1,3 +1,12 @@
+"""List-scheduling simulation of the search batch's tail ("The tail").  4096 persistent
+searchers take queries from a counter; a query costs its expansions + 10 (init and descent), in
+expansion units.  Compared: batch order, longest-first (LPT), and suspending a query after q
+expansions (its continuation queued behind the fresh queries or ahead of them, re-queued while fresh
+queries remain or always).  The per-query expansion counts come from the oracle's search on a
+host-built SIFT-like graph (300k rows, ef 70, 10k queries), saved to /tmp/sift_cost.npy by:
+  g = native.Graph.build(base, 0, 32, 100, 8, 100); view = oracle.IndexView(...);
+  cost = [view.search(q, 10, 70, with_counters=True)[2][1] for q in queries]
+"""
 import numpy as np, heapq, collections, sys
 c=np.load('/tmp/sift_cost.npy').astype(float)
 W=4096; init=10.0
