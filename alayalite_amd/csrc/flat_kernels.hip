@@ -658,18 +658,25 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
         }
       }
     };
-    float4 stage[kPerThread];
-    load_tile(r0, stage);
-    store_tile(0, stage);
+    // K <= 128: row tiles are loaded two ahead (tile s + 2 while tile s is contracted, tile s + 1
+    // waits in registers), so a tile's loads have a whole step plus the staging wait to land; wider
+    // rows load one ahead (the registers of a second tile would spill)
+    constexpr bool kDeep = K <= 128;
+    float4 stage_a[kPerThread], stage_b[kDeep ? kPerThread : 1];
+    load_tile(r0, stage_a);
+    store_tile(0, stage_a);
+    if (kDeep && ntiles > 1) load_tile(r0 + kTile, stage_a);
     __syncthreads();  // the only block-wide barrier: tile 0 staged, sync words zeroed
     const bool diag = p.merge_count != nullptr;
     uint64_t t_slot = 0, t_staged = 0;
     const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
     int slot = 0;
-    for (int s = 0; s < ntiles; ++s) {
+    // one step: contract tile s (LDS buffer s & 1), publish it, stage tile s + 1 from `next` (kDeep:
+    // while tile s + 2 loads into `ahead`); false = aborted
+    auto step = [&](int s, float4 (&next)[kPerThread], float4 (&ahead)[kPerThread]) -> bool {
       const int buf = s & 1;
-      const bool more = s + 1 < ntiles;
-      if (more) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 1), stage);
+      if (kDeep && s + 2 < ntiles) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 2), ahead);
+      if (!kDeep && s + 1 < ntiles) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 1), next);
       f32x16 c = {};
       const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
 #pragma unroll
@@ -682,29 +689,36 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
       }
       // ring slot s % kD is free once the consumers have read tile s - kD
       const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-      bool free_slot = true;
 #pragma unroll
       for (int c2 = 0; c2 < kCons; ++c2)
-        if (s >= kD && free_slot &&
-            !lds_wait_ge(&consumed[w * kCons + c2], static_cast<uint32_t>(s + 1 - kD), abort, p.spin_limit))
-          free_slot = false;
-      if (!free_slot) break;
+        if (s >= kD && !lds_wait_ge(&consumed[w * kCons + c2], static_cast<uint32_t>(s + 1 - kD), abort, p.spin_limit))
+          return false;
       if (diag) t_slot += __builtin_amdgcn_s_memtime() - tw;
       float *out = cx + ((slot * 4 + w) * 16) * 64 + lane;
 #pragma unroll
       for (int r = 0; r < 16; ++r) out[r * 64] = c[r];
       lds_publish(&published[w], static_cast<uint32_t>(s + 1));
       slot = slot + 1 == kD ? 0 : slot + 1;
-      if (more) {
+      if (s + 1 < ntiles) {
         // every producer has finished this step's MFMAs on `buf` before any stages tile s + 2 into
         // it, and tile s + 1 is complete before any reads it
-        store_tile(buf ^ 1, stage);
+        store_tile(buf ^ 1, next);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         if (lane == 0) __hip_atomic_fetch_add(staged, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint64_t tb = diag ? __builtin_amdgcn_s_memtime() : 0;
-        if (!lds_wait_ge(staged, static_cast<uint32_t>(4 * (s + 1)), abort, p.spin_limit)) break;
-        if (diag) t_staged += __builtin_amdgcn_s_memtime() - tb;
+        const uint64_t tb2 = diag ? __builtin_amdgcn_s_memtime() : 0;
+        if (!lds_wait_ge(staged, static_cast<uint32_t>(4 * (s + 1)), abort, p.spin_limit)) return false;
+        if (diag) t_staged += __builtin_amdgcn_s_memtime() - tb2;
       }
+      return true;
+    };
+    if constexpr (kDeep) {
+      for (int s = 0; s < ntiles; s += 2) {
+        if (!step(s, stage_a, stage_b)) break;
+        if (s + 1 < ntiles && !step(s + 1, stage_b, stage_a)) break;
+      }
+    } else {
+      for (int s = 0; s < ntiles; ++s)
+        if (!step(s, stage_a, stage_a)) break;
     }
     if (diag && lane == 0) {  // diagnostics: producer rows after the consumers' (tools/flat_diag.py)
       unsigned long long *st =
