@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 OUT=${1:-gpurun_out/traffic.json}
 shift
 EF=${EF:-400}
-ARGS="--ef $EF --steps 5 --warmup 1 --no-cpu-baseline --builder gpu $*"
+ARGS="--ef $EF --steps 5 --warmup 1 --no-cpu-baseline --no-tail-probe --builder gpu $*"
 rm -rf gpurun_out/pmc_*
 IFS=';' read -ra PASSES <<< "${GROUPS_PMC:-FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum}"
 for grp in "${PASSES[@]}"; do
