@@ -419,6 +419,9 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.sq_min = ix->sq_min.as<float>();
     p.sq_max = ix->sq_max.as<float>();
   }
+  // diagnostics flags (read again by prepare_spill); bit 8 selects the prefetch-check kernel, so it
+  // must be known before the occupancy probes
+  if (const char *e = std::getenv("ALAYA_SPILL_FLAGS")) p.spill_flags = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   // the visited second level: spill table or bitset
   p.stab_log2 = spill_table_log2(p.sq8_order, std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2))), ef);
   // waves per workgroup: never more than the batch needs

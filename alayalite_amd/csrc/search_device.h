@@ -747,6 +747,20 @@ __device__ __forceinline__ void stab_store(const Visited &vs, uint32_t entry, ui
   __hip_atomic_store(vs.stab + entry, static_cast<uint16_t>(code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Order the wave's earlier spill-table stores (and bitset atomics) before its later bucket reads.
+// Every access to a slot's table comes from the one wave that owns the slot, from one CU, so the
+// order needed is the workgroup's: the seq_cst workgroup fence is the language-level guarantee (no
+// compiler may move a load above it; in LLVM's AMDGPU memory model the CU then performs the wave's
+// memory operations in order, so gfx950 emits no instruction for it), and s_waitcnt(0) makes the
+// stores complete at L2 -- where the agent-scope reads look -- before the reads are issued.  An
+// agent-scope fence would be wrong here: on gfx950 it writes back and invalidates the whole L2
+// (buffer_wbl2 / buffer_inv sc1) for an order that never leaves the wave.
+__device__ __forceinline__ void stab_order() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
 // found: the bucket holds `code`; occ: entries in use (= the first free position)
 __device__ __forceinline__ void stab_scan(uint64_t lo, uint64_t hi, uint32_t code, bool &found, uint32_t &occ) {
   found = false;
@@ -768,7 +782,7 @@ __device__ __forceinline__ bool stab_visit(Visited &vs, uint32_t v, bool act, bo
   uint32_t home = 0, code = 0;
   stab_key(vs, v, home, code);
   if (!pre_ok) {
-    __builtin_amdgcn_s_waitcnt(0);  // every earlier store of this wave has landed in L2
+    stab_order();
     if (act) stab_load(vs, home, lo, hi);
   }
   bool found;
@@ -942,8 +956,9 @@ __device__ __forceinline__ void visit_end(Visited &vs) {
     for (uint64_t w = lane; w < vs.n_words; w += 64)
       __hip_atomic_store(&vs.bits[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __threadfence_block();  // the clearing stores land before the slot's next query sets bits
-  __builtin_amdgcn_s_waitcnt(0);  // (and before its agent-scope spill-table reads)
+  // the clearing stores land before the slot's next query sets bits (and before its agent-scope
+  // spill-table reads)
+  stab_order();
   vs.spilled = false;
 }
 

@@ -62,7 +62,8 @@ struct SearchParams {
   uint16_t *spill_table;  // slots x 2^stab_log2 entries
   uint32_t stab_log2;
   uint32_t stab_rbits;    // <= 15
-  uint32_t spill_flags;   // diagnostics (ALAYA_SPILL_FLAGS): bit 0 = no second-level prefetch
+  uint32_t spill_flags;   // diagnostics (ALAYA_SPILL_FLAGS): bit 0 = no second-level prefetch, bit 2 =
+                          // prefetch after the rows land, bit 8 = the prefetch-check kernel (kDiag 2)
   uint64_t *stamps;       // nullable: diagnostic per-phase cycle counts, nq x 8
   // SQ8 search space (SQ8Space, space/sq8_space.hpp): traversal distances on uint8 codes
   int sq8_order;          // 0 = f32 RawSpace search; 2 = AVX-512 SQ8 order; 1 = AVX2 SQ8 order

@@ -264,17 +264,21 @@ __device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, c
 // --------------------------------------------------------------------------------------------
 // The search kernel.
 // --------------------------------------------------------------------------------------------
-// kStamp: diagnostic build that accumulates s_memtime cycles per phase into p.stamps (nq x 8):
+// kDiag: 0 = the search; 1 = diagnostic build that accumulates s_memtime cycles per phase into
+// p.stamps (nq x 8):
 // [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
-// [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] prefetch hits.
+// [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] prefetch hits;
+// 2 = the spill-table prefetch check (ALAYA_SPILL_FLAGS bit 8: every bucket read one expansion ahead
+// is compared with a re-read at its use, and a stale one marks the query's counters).
 // A workgroup holds blockDim.x / 64 waves (1 for f32 rows, up to 4 for SQ8, which share the
 // quantizer's scale / min); each wave is an independent persistent searcher with its own visited
 // spill slot.  After fill_shared the waves never synchronise again.
-template <bool kIP, int kChunks, bool kStamp, int kSpace = 0>
+template <bool kIP, int kChunks, int kDiag, int kSpace = 0>
 __global__ void __launch_bounds__(256)
     __attribute__((amdgpu_waves_per_eu(search_min_waves<kChunks, kSpace>() ? search_min_waves<kChunks, kSpace>() : 1,
                                        8))) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool kStamp = kDiag == 1;
   const int lane = lane_id();
   const int wave = static_cast<int>(threadIdx.x >> 6);
   const Lds L = carve_lds<kSpace>(p, smem, wave);
@@ -355,7 +359,26 @@ __global__ void __launch_bounds__(256)
         }
       }
       if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin<space_tab<kSpace>()>(vs);
+      if constexpr (kDiag == 2 && space_tab<kSpace>()) {
+        // diagnostics (tests/test_sq8_spill.py): the buckets read one expansion ahead must equal the
+        // table as it is now; a stale one marks the query's counters
+        if (u == pre_u && vs.spilled && vs.stab != nullptr) {
+          stab_order();
+          uint32_t home, code;
+          stab_key(vs, v, home, code);
+          uint64_t lo2 = 0ull, hi2 = 0ull;
+          if (act) stab_load(vs, home, lo2, hi2);
+          if (ballot(act && (lo2 != pre_lo || hi2 != pre_hi))) n_hops_up |= 0x40000000u;
+        }
+      }
       const bool fresh = visit<space_tab<kSpace>()>(vs, v, act, kSpillPrefetch && u == pre_u, pre_lo, pre_hi);
+      if constexpr (kSpillPrefetch) {
+        // the pred_v load below must issue after this visit's spill-table stores and bitset atomics:
+        // the second-level prefetch's wait for pred_v is its wait for them (vmcnt retires in issue
+        // order), so no compiler may move the load above them
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+      }
       // consumed: the prefetched state describes the table only up to this visit's stores, so it
       // is never reused (an expansion without fresh neighbours skips the prefetch below, and the
       // next pop must not take this one for its own); zeroed so it is not live across the
@@ -380,9 +403,10 @@ __global__ void __launch_bounds__(256)
       wave_sync();
       // The second-level prefetch of the predicted next expansion goes out right after this
       // expansion's first row pass is issued, so its latency overlaps the rows'.  It needs pred_v,
-      // which was loaded after this visit's stores and atomics and before the rows: the wait for
-      // pred_v (vmcnt counts loads, stores and atomics in issue order) is the wait for them too, so
-      // the prefetch reads the table as this visit left it.
+      // which was loaded after this visit's stores and atomics (the barrier after the visit pins
+      // that order) and before the rows: the wait for pred_v (vmcnt counts loads, stores and atomics
+      // in issue order) is the wait for them too, so the prefetch reads the table as this visit left
+      // it (ALAYA_SPILL_FLAGS bit 8 checks every prefetched bucket against a re-read).
       space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd, [&]() {
         if constexpr (kSpillPrefetch) {
           if (vs.spilled && pred != kEmpty && !(p.spill_flags & 1u)) {
@@ -575,29 +599,33 @@ hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream
   return hipGetLastError();
 }
 
-template <bool kIP, int kChunks, bool kStamp = false, int kSpace = 0>
+template <bool kIP, int kChunks, int kDiag = 0, int kSpace = 0>
 static const void *kernel_ptr() {
-  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kStamp, kSpace>);
+  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kDiag, kSpace>);
 }
 
 template <int kSpace>
-static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped) {
+static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped, bool check) {
   const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
-  if (stamped && chunks == 24) return ip ? kernel_ptr<true, 24, true, kSpace>() : kernel_ptr<false, 24, true, kSpace>();
-  if (chunks == 4) return ip ? kernel_ptr<true, 4, false, kSpace>() : kernel_ptr<false, 4, false, kSpace>();
-  if (chunks == 24) return ip ? kernel_ptr<true, 24, false, kSpace>() : kernel_ptr<false, 24, false, kSpace>();
-  if (chunks == 30) return ip ? kernel_ptr<true, 30, false, kSpace>() : kernel_ptr<false, 30, false, kSpace>();
-  return ip ? kernel_ptr<true, 0, false, kSpace>() : kernel_ptr<false, 0, false, kSpace>();
+  if (stamped && chunks == 24) return ip ? kernel_ptr<true, 24, 1, kSpace>() : kernel_ptr<false, 24, 1, kSpace>();
+  if constexpr (kSpace == 2) {  // the spill-table prefetch check (config 5's d = 768 and d = 960)
+    if (check && chunks == 24) return ip ? kernel_ptr<true, 24, 2, kSpace>() : kernel_ptr<false, 24, 2, kSpace>();
+    if (check && chunks == 30) return ip ? kernel_ptr<true, 30, 2, kSpace>() : kernel_ptr<false, 30, 2, kSpace>();
+  }
+  if (chunks == 4) return ip ? kernel_ptr<true, 4, 0, kSpace>() : kernel_ptr<false, 4, 0, kSpace>();
+  if (chunks == 24) return ip ? kernel_ptr<true, 24, 0, kSpace>() : kernel_ptr<false, 24, 0, kSpace>();
+  if (chunks == 30) return ip ? kernel_ptr<true, 30, 0, kSpace>() : kernel_ptr<false, 30, 0, kSpace>();
+  return ip ? kernel_ptr<true, 0, 0, kSpace>() : kernel_ptr<false, 0, 0, kSpace>();
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic) {
-  if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped);
-  if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped);
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic, bool check) {
+  if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped, check);
+  if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped, false);
   const uint32_t chunks = (!generic && dim % 32 == 0) ? dim / 32 : 0;  // generic order: the runtime-d kernel
   if (stamped) {
-    if (chunks == 30) return ip ? kernel_ptr<true, 30, true>() : kernel_ptr<false, 30, true>();
-    if (chunks == 4) return ip ? kernel_ptr<true, 4, true>() : kernel_ptr<false, 4, true>();
-    return ip ? kernel_ptr<true, 0, true>() : kernel_ptr<false, 0, true>();
+    if (chunks == 30) return ip ? kernel_ptr<true, 30, 1>() : kernel_ptr<false, 30, 1>();
+    if (chunks == 4) return ip ? kernel_ptr<true, 4, 1>() : kernel_ptr<false, 4, 1>();
+    return ip ? kernel_ptr<true, 0, 1>() : kernel_ptr<false, 0, 1>();
   }
 #define ALAYA_CASE(C)                                                        \
   if (chunks == C) return ip ? kernel_ptr<true, C>() : kernel_ptr<false, C>();
@@ -612,7 +640,8 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_or
 }
 
 hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic,
+                                        (p.spill_flags & 256u) != 0);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64 * waves), args, lds, stream);
@@ -631,7 +660,8 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 }
 
 hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu) {
-  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic);
+  const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic,
+                                        (p.spill_flags & 256u) != 0);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * waves, lds);
 }
 

@@ -420,6 +420,11 @@ def run_flat(args):
     flops = 2.0 * n * nq * dim
     tf = flops / (ms * 1e-3) / 1e12
     scan = flat_scan_kernel_name(dim)
+    # the roofline is the issued contraction's own MFMA peak: the default bf16 hi/lo split issues 3
+    # bf16 products per f32 product, so its ceiling is the dense bf16 peak (16 x 157.3 TF) / 3; the f32
+    # contraction (ALAYA_FLAT_F32) runs at the 157.3 TF f32 MFMA peak
+    f32_contraction = bool(os.environ.get("ALAYA_FLAT_F32"))
+    mfma_peak = 157.3 if f32_contraction else round(16 * 157.3 / 3, 1)
     # HBM traffic of the scan from the committed PMC passes on this workload and kernel
     # (tools/run_pmc_flat.sh; latest round first)
     import glob
@@ -454,20 +459,20 @@ def run_flat(args):
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": f"flat-{n // 1000}k-{dim}-l2-{nq}q", "n_base": n, "n_queries": nq, "dim": dim, "k": K,
                    "flagged_queries": n_flag, "exact_vs_f64_sample": f"{ok}/{len(sample)}"},
-        "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
-                     "frac": round(tf / 157.3, 4),
+        "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": mfma_peak, "unit": "TFLOP/s",
+                     "frac": round(tf / mfma_peak, 4),
                      "traffic": round(traffic["traffic_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1) if traffic else None,
                      "traffic_unit": f"GB/s (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE of {scan})",
                      "traffic_bytes_per_launch": int(traffic["traffic_bytes_per_launch"]) if traffic else None,
                      "traffic_source": tsrc,
                      "kernel": f"{scan}+flat_merge_kernel",
                      "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops,
-                     # the default contraction issues 3 bf16 MFMAs per f32 product (hi/lo split):
-                     # its own ceiling is the 2.5 PF bf16 peak / 3, which the scan is far from --
-                     # candidate handling, not the MFMA pipe, sets the time
-                     "contraction": "f32" if os.environ.get("ALAYA_FLAT_F32") else "bf16x3",
-                     "split_ceiling": None if os.environ.get("ALAYA_FLAT_F32") else 833.3,
-                     "split_frac": None if os.environ.get("ALAYA_FLAT_F32") else round(tf / 833.3, 4)},
+                     # achieved = algorithmic f32 products (2 n nq d) / kernel time; peak = the issued
+                     # contraction's dense MFMA peak (bf16x3: 2516.8 TF / 3; f32: 157.3 TF)
+                     "contraction": "f32" if f32_contraction else "bf16x3",
+                     "peak_source": ("f32 MFMA dense peak (MI355X_MICROARCH.md)" if f32_contraction else
+                                     "bf16 MFMA dense peak 16 x 157.3 TF / 3 bf16 products per f32 product "
+                                     "(MI355X_MICROARCH.md)")},
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -43,8 +43,13 @@ def test_fixed_d_f32_expansion_loops_restore_no_spilled_sgpr(census, metric, chu
 
 # The AVX-512-order SQ8 kernels carry the spill table (round 4: flush, bucket prefetch, bitset third
 # level), whose uniform state costs SGPR restores per expansion -- 12-31 v_readlane against ~12k
-# cycles per expansion at config 5.  The AVX2-order kernels keep the bitset (0-2 restores).
-SQ8_RESTORE_BUDGET = {"sq8-avx512": 40, "sq8-avx2": 4}
+# cycles per expansion at config 5 (measured on this image's hipcc: 12 in config 5's 768-d IP
+# kernel, 31 in the others).  The AVX2-order kernels keep the bitset (0-4 restores).  Budgets are
+# the measured maxima plus a small margin, so a regression shows up here first.
+SQ8_RESTORE_BUDGET = {"sq8-avx512": 34, "sq8-avx2": 4}
+# scratch bytes the AVX-512-order SQ8 kernels may use (held to 128 VGPRs: a value or two live across
+# the query loop, stored at kernel entry and loaded after it -- never inside an expansion)
+SQ8_SCRATCH_BYTES = {"ip chunks=24": 12, "l2 chunks=24": 0, "ip chunks=30": 28, "l2 chunks=30": 12}
 
 
 @pytest.mark.parametrize("space", ["sq8-avx512", "sq8-avx2"])
@@ -65,7 +70,8 @@ def test_register_budgets(census):
         if "stamp=0" in k:  # (the stamped kernels are diagnostics builds)
             assert r["scratch_ops_in_expansion_loops"] == 0, k
         if "sq8-avx512" in k and "chunks=0" not in k and "stamp=0" in k:
-            assert r.get("ScratchSize", 0) <= 32 and r["scratch_ops_total"] <= 8, (k, r.get("ScratchSize"))
+            budget = SQ8_SCRATCH_BYTES.get(k.split(" stamp")[0], 0)
+            assert r.get("ScratchSize", 0) <= budget and r["scratch_ops_total"] <= 8, (k, r.get("ScratchSize"))
         elif "stamp=0" in k:
             assert r.get("ScratchSize", 0) == 0, k
     assert census["ip chunks=24 stamp=0 space=sq8-avx512"]["NumVgprs"] <= 128

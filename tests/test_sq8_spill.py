@@ -100,3 +100,18 @@ def test_fixed_d_sq8_spilled_second_levels(native, setups, monkeypatch, spill_ta
     if spill_table is not None:
         monkeypatch.setenv("ALAYA_SPILL_TABLE", spill_table)
     _run(native, setups(768, 1, 2), 2, 1, 340, visited_mode, 8)
+
+
+@pytest.mark.parametrize("ef", [40, 340])
+@pytest.mark.parametrize("waves", ["1", "4"])
+@pytest.mark.parametrize("metric", [1, 0])
+@pytest.mark.parametrize("d", [768, 960])
+def test_spill_table_prefetch_matches_a_reread(native, setups, monkeypatch, d, metric, waves, ef):
+    """The order the spill-table prefetch relies on, checked at run time: ALAYA_SPILL_FLAGS bit 8 runs
+    the kDiag = 2 kernel, which re-reads every bucket it read one expansion ahead, at the visit that
+    uses it (after a workgroup fence and s_waitcnt(0)), and sets bit 30 of the query's n_hops_upper
+    counter when any differs -- so a stale prefetch (a bucket read before the previous visit's
+    stores landed) fails the counter comparison with the restatement."""
+    monkeypatch.setenv("ALAYA_SEARCH_WAVES", waves)
+    monkeypatch.setenv("ALAYA_SPILL_FLAGS", "256")
+    _run(native, setups(d, metric, 2), 2, metric, ef)

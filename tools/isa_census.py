@@ -38,7 +38,7 @@ def compile_asm(src: str, extra: list[str]) -> str:
 
 
 def demangle(name: str) -> str:
-    m = re.search(r"hnsw_search_kernelILb(\d)ELi(\d+)ELb(\d)ELi(\d)E", name)
+    m = re.search(r"hnsw_search_kernelILb(\d)ELi(\d+)EL[bi](\d)ELi(\d)E", name)
     if not m:
         return name
     ip, chunks, stamp, space = m.groups()
