@@ -123,6 +123,10 @@ struct alaya_index {
   size_t overflow_clean = 0;  // leading bytes of `overflow` known to be zero (kernels leave it clean)
   size_t stab_clean = 0;      // the same for the spill tables
   uint32_t hash_log2_override = 0;
+  int helpers_mode = -1;          // distance helpers: -1 automatic, 0 off, 1 on (alaya_index_set_helpers)
+  DevBuf help_stats;              // per searcher of the last helper launch: (memo distances, memo expansions)
+  uint64_t help_stats_slots = 0;
+  uint32_t last_grid = 0, last_waves = 0;  // the last search launch's workgroups and waves per workgroup
   int visited_mode_override = 0;  // 0 auto, 1 compact 16-bit slots, 2 wide 32-bit slots,
                                   // 3 compact with probes capped at 2 (exercises the probe spill)
   int num_cus = 0;
@@ -301,6 +305,21 @@ uint64_t max_search_waves_per_cu() {
   return kMaxSearchWavesPerCu;
 }
 
+// Distance helpers (search kernel kMode 4, search_has_helpers): with helpers every search runs 4-wave
+// workgroups, and a batch smaller than the resident searchers still fills the CUs, so each workgroup
+// has idle waves to help from the start.  Automatic policy, from the measurements in DESIGN.md
+// (round 5, "distance helpers"): on for the SQ8 kernels (config 5: 1k queries 3.75 -> 3.54 ms, 10k
+// 9.60 -> 9.53 ms); for the small-row f32 kernels only when the batch outnumbers the resident
+// searchers, i.e. for its tail (SIFT-shaped 10k 1.192 -> 1.138 ms; at 1k the helper layout costs more
+// than it saves: 0.536 -> 0.583 ms).  alaya_index_set_helpers and ALAYA_HELPERS=0/1 override it.
+bool helpers_requested(const alaya_index *ix, const SearchParams &p, uint64_t nq, uint64_t cus) {
+  if (const char *e = std::getenv("ALAYA_HELPERS")) return std::atoi(e) != 0;  // A/B override
+  if (ix->helpers_mode >= 0) return ix->helpers_mode > 0;
+  if (std::getenv("ALAYA_SEARCH_WAVES")) return false;  // a forced workgroup shape (diagnostics, tests)
+  if (p.sq8_order == 2) return true;
+  return nq > max_search_waves_per_cu() * cus;
+}
+
 uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef, int W = 1) {
   const uint32_t lbits = std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2)));
   const int mode = ix->visited_mode_override;  // 0 auto, 1 compact, 2 wide, 3 compact + short probes
@@ -337,7 +356,8 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     // profiles/r04/spill_table/c5_first_level_size_threshold.log).  LDS then bounds nothing.
     return set_mode(7, false);
   }
-  const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0);
+  const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0) +
+                        (p.help ? alaya_amd::kHelpBoardBytes : 0);
   const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
   // the register-bound residency, probed with a 4 KB table -- or with the smallest table when a
   // spill table is the second level (a spill then costs a flush and prefetched bucket reads, not a
@@ -347,8 +367,9 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + (stab ? 1024 : 4096)), &vgpr_blocks),
             "occupancy");
   const uint64_t vgpr_waves = static_cast<uint64_t>(std::max(1, vgpr_blocks)) * W;
-  const uint64_t want = (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
   const uint64_t max_waves = std::max<uint64_t>(W, max_search_waves_per_cu());
+  // with helpers a small batch still fills the CUs (the waves without a query help)
+  const uint64_t want = p.help ? max_waves : (nq + ix->num_cus - 1) / std::max(1, ix->num_cus);
   uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>({vgpr_waves, want, max_waves}));
   const uint32_t cap = ceil_log2(48ull * ef);
   // table bytes per wave when `w` waves share a CU in workgroups of W
@@ -380,6 +401,22 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
     if (mode == 1 || mode == 3) throw ArgError("compact visited table cannot encode ids of this index");
   }
   return set_mode(pick(4, 15), false);
+}
+
+// CUs a launch on `s` may use: all of the device's, unless the stream carries a CU mask
+// (alaya_stream_create_reserving: the persistent grid is sized to the CUs left to it, so none of its
+// workgroups waits for a CU that another stream's kernels -- the shard exchange's -- keep).
+int stream_cus(const alaya_index *ix, hipStream_t s) {
+  if (s == nullptr) return ix->num_cus;
+  uint32_t mask[32] = {};
+  const uint32_t words = static_cast<uint32_t>((ix->num_cus + 31) / 32);
+  if (words > 32 || hipExtStreamGetCUMask(s, words, mask) != hipSuccess) {
+    (void)hipGetLastError();
+    return ix->num_cus;
+  }
+  int c = 0;
+  for (uint32_t w = 0; w < words; ++w) c += __builtin_popcount(mask[w]);
+  return c > 0 && c <= ix->num_cus ? c : ix->num_cus;
 }
 
 void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t ef,
@@ -424,22 +461,82 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
   if (const char *e = std::getenv("ALAYA_SPILL_FLAGS")) p.spill_flags = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   // the visited second level: spill table or bitset
   p.stab_log2 = spill_table_log2(p.sq8_order, std::max<uint32_t>(1, ceil_log2(std::max<uint64_t>(ix->n, 2))), ef);
-  // waves per workgroup: never more than the batch needs
-  int W = search_waves(p);
-  while (W > 1 && static_cast<uint64_t>(W) > nq) W /= 2;
-  p.hash_log2 = size_visited(ix, p, nq, ef, W);
-  const bool compact = p.vis_rbits != alaya_amd::kVisWide;
-  p.wave_lds = static_cast<uint32_t>(alaya_amd::search_wave_lds_bytes(ix->stride, ef, p.hash_log2, compact));
-  const size_t lds = alaya_amd::search_shared_lds_bytes(ix->stride, sq8) + static_cast<size_t>(W) * p.wave_lds;
+  // distance helpers (4-wave workgroups; a helper's memo of 4 x R entries lives in its pool and
+  // visited table, checked below)
+  p.help = (helpers_requested(ix, p, nq, static_cast<uint64_t>(stream_cus(ix, stream))) && ix->R <= 64 &&
+            alaya_amd::search_has_helpers(ix->dim, p.sq8_order, ix->generic)) ? 1u : 0u;
+  if (const char *e = std::getenv("ALAYA_HELP_FLAGS")) p.help_flags = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
+  // Wide f32 rows (d = 768 / 960) run one searcher per SIMD; a batch a little larger than that
+  // (config 4's S = 1 layout: 1,250 queries per rank on 1,024 searchers) would leave most of a
+  // second round idle, so it runs the two-waves-per-SIMD kernel instead (one row per lane group):
+  // GIST-shaped 1M, ef 373, 1,250 queries 8.92 -> 7.44 ms, <= 1,024 queries equal, 2,048 and more
+  // slower (profiles/r05/gist_rounds/).  ALAYA_TWO_WAVES = 0 / 1 forces it off / on.
+  p.two_waves = 0;
+  if (!p.help && d_stamps == nullptr && alaya_amd::search_has_two_waves(ix->dim, p.sq8_order, ix->generic)) {
+    const char *e = std::getenv("ALAYA_TWO_WAVES");
+    const int force = e ? std::atoi(e) : -1;
+    if (force == 1) {
+      p.two_waves = 1;
+    } else if (force != 0) {
+      int b1 = 0;
+      const size_t probe = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 12, true);
+      hip_check(alaya_amd::search_occupancy(p, 1, probe, &b1), "occupancy");
+      const uint64_t resident1 = static_cast<uint64_t>(std::max(1, b1)) * static_cast<uint64_t>(stream_cus(ix, stream));
+      p.two_waves = (nq > resident1 && 2 * nq <= 3 * resident1) ? 1u : 0u;
+    }
+  }
+  // waves per workgroup: never more than the batch needs (helpers: always 4).  A plan with helpers
+  // that does not fit (the memo, or four waves' LDS with a forced large visited table) falls back
+  // to the search without them.
+  int W = 1;
+  size_t lds = 0;
+  for (;;) {
+    W = p.help ? 4 : search_waves(p);
+    while (!p.help && W > 1 && static_cast<uint64_t>(W) > nq) W /= 2;
+    p.hash_log2 = size_visited(ix, p, nq, ef, W);
+    const bool compact = p.vis_rbits != alaya_amd::kVisWide;
+    p.wave_lds = static_cast<uint32_t>(alaya_amd::search_wave_lds_bytes(ix->stride, ef, p.hash_log2, compact));
+    bool fits = true;
+    if (p.help) {
+      // the memo (W searchers x 3 requests x R entries of 8 bytes) overlays the memo wave's query
+      // vector, or else its pool and visited table
+      const size_t need = static_cast<size_t>(W) * alaya_amd::kHelpMemoSlots * ix->R * 8;
+      const size_t q_bytes = static_cast<size_t>(ix->stride) * 4;
+      if (q_bytes >= need) {
+        p.memo_off = 0;
+      } else if (p.wave_lds - (q_bytes + 3 * 64 * 4) >= need) {
+        p.memo_off = static_cast<uint32_t>(q_bytes + 3 * 64 * 4);
+      } else {
+        fits = false;
+      }
+    }
+    lds = alaya_amd::search_shared_lds_bytes(ix->stride, sq8) + static_cast<size_t>(W) * p.wave_lds +
+          (p.help ? alaya_amd::kHelpBoardBytes : 0);
+    if (p.help && (!fits || lds > kLdsPerCu)) {
+      p.help = 0;
+      continue;
+    }
+    break;
+  }
   if (lds > kLdsPerCu) throw ArgError("ef / dim too large for the LDS budget");
   int per_cu = 0;
   hip_check(alaya_amd::search_occupancy(p, W, lds, &per_cu), "occupancy");
   per_cu = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(per_cu, max_search_waves_per_cu() / W)));
-  const uint64_t blocks_needed = (nq + W - 1) / W;
-  const uint64_t grid64 = std::min<uint64_t>(blocks_needed, static_cast<uint64_t>(per_cu) * ix->num_cus);
+  // with helpers the grid fills the CUs whatever the batch (idle waves help from the start)
+  const uint64_t cus = static_cast<uint64_t>(stream_cus(ix, stream));
+  const uint64_t blocks_needed = p.help ? static_cast<uint64_t>(per_cu) * cus : (nq + W - 1) / W;
+  const uint64_t grid64 = std::min<uint64_t>(blocks_needed, static_cast<uint64_t>(per_cu) * cus);
   const int grid = static_cast<int>(std::max<uint64_t>(1, grid64));
   scratch_acquire(ix, stream);
   prepare_spill(ix, p, static_cast<uint64_t>(grid) * W, stream);
+  ix->last_grid = static_cast<uint32_t>(grid);
+  ix->last_waves = static_cast<uint32_t>(W);
+  ix->help_stats_slots = 0;
+  if (p.help) {
+    ix->help_stats_slots = static_cast<uint64_t>(grid) * W;
+    ix->help_stats.reserve(ix->help_stats_slots * 12);
+    p.help_stats = ix->help_stats.as<uint32_t>();
+  }
   ix->work.reserve(4);
   p.work_counter = ix->work.as<uint32_t>();
   hip_check(hipMemsetAsync(p.work_counter, 0, 4, stream), "hipMemsetAsync");
@@ -1713,6 +1810,71 @@ int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots) {
     if (!ix) throw ArgError("null index");
     if (log2_slots != 0 && (log2_slots < 6 || log2_slots > 16)) throw ArgError("log2_slots must be 0 or 6..16");
     ix->hash_log2_override = log2_slots;
+  });
+}
+
+int alaya_stream_create_reserving(int device, uint32_t reserved_cus, void **stream) {
+  return guarded([&] {
+    if (!stream) throw ArgError("null stream pointer");
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    hipDeviceProp_t prop;
+    hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+    const uint32_t n = static_cast<uint32_t>(prop.multiProcessorCount);
+    if (reserved_cus >= n) throw ArgError("reserved_cus must leave at least one CU");
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (uint32_t c = 0; c < n; ++c) mask[c / 32] |= 1u << (c % 32);
+    // the reserved CUs spread evenly over the CU numbering (so over the XCDs)
+    for (uint32_t r = 0; r < reserved_cus; ++r) {
+      const uint32_t c = static_cast<uint32_t>((static_cast<uint64_t>(r) * n) / reserved_cus);
+      mask[c / 32] &= ~(1u << (c % 32));
+    }
+    hipStream_t s = nullptr;
+    hip_check(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()),
+              "hipExtStreamCreateWithCUMask");
+    *stream = s;
+  });
+}
+
+int alaya_stream_destroy(void *stream) {
+  return guarded([&] {
+    if (stream) hip_check(hipStreamDestroy(static_cast<hipStream_t>(stream)), "hipStreamDestroy");
+  });
+}
+
+int alaya_index_last_launch(const alaya_index *ix, uint32_t *workgroups, uint32_t *waves_per_group) {
+  return guarded([&] {
+    if (!ix) throw ArgError("null index");
+    if (workgroups) *workgroups = ix->last_grid;
+    if (waves_per_group) *waves_per_group = ix->last_waves;
+  });
+}
+
+int alaya_index_set_helpers(alaya_index *ix, int mode) {
+  return guarded([&] {
+    if (!ix) throw ArgError("null index");
+    if (mode < -1 || mode > 1) throw ArgError("helpers mode must be -1 (automatic), 0 (off) or 1 (on)");
+    ix->helpers_mode = mode;
+  });
+}
+
+int alaya_index_help_stats(alaya_index *ix, uint64_t *memo_dists, uint64_t *memo_expansions, uint64_t *helper_rows) {
+  return guarded_scratch(ix, [&] {
+    if (!ix) throw ArgError("null index");
+    uint64_t m = 0, x = 0, r = 0;
+    if (ix->help_stats_slots) {
+      set_device(ix);
+      scratch_drain(ix);
+      std::vector<uint32_t> h(3 * ix->help_stats_slots);
+      hip_check(hipMemcpy(h.data(), ix->help_stats.ptr, h.size() * 4, hipMemcpyDeviceToHost), "D2H");
+      for (uint64_t i = 0; i < ix->help_stats_slots; ++i) {
+        m += h[3 * i];
+        x += h[3 * i + 1];
+        r += h[3 * i + 2];
+      }
+    }
+    if (memo_dists) *memo_dists = m;
+    if (memo_expansions) *memo_expansions = x;
+    if (helper_rows) *helper_rows = r;
   });
 }
 

@@ -281,6 +281,17 @@ class PyIndexInterface {
   }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
   void set_visited_mode(int m) { check(alaya_index_set_visited_mode(ix_, m)); }
+  void set_helpers(int m) { check(alaya_index_set_helpers(ix_, m)); }
+  py::tuple last_launch() {
+    uint32_t g = 0, w = 0;
+    check(alaya_index_last_launch(ix_, &g, &w));
+    return py::make_tuple(g, w);
+  }
+  py::tuple help_stats() {
+    uint64_t m = 0, x = 0, r = 0;
+    check(alaya_index_help_stats(ix_, &m, &x, &r));
+    return py::make_tuple(m, x, r);
+  }
   // SQ8 batch_search rerank: 1 = the reference's PyIndex::rerank (default), 2 = corrected (whole ef pool)
   void set_rerank_mode(int m) {
     if (m != 1 && m != 2) throw std::invalid_argument("rerank mode must be 1 (reference) or 2 (corrected)");
@@ -848,6 +859,17 @@ class DeviceIndex {
   }
   void set_hash_log2(uint32_t v) { check(alaya_index_set_hash_log2(ix_, v)); }
   void set_visited_mode(int m) { check(alaya_index_set_visited_mode(ix_, m)); }
+  void set_helpers(int m) { check(alaya_index_set_helpers(ix_, m)); }
+  py::tuple last_launch() {
+    uint32_t g = 0, w = 0;
+    check(alaya_index_last_launch(ix_, &g, &w));
+    return py::make_tuple(g, w);
+  }
+  py::tuple help_stats() {
+    uint64_t m = 0, x = 0, r = 0;
+    check(alaya_index_help_stats(ix_, &m, &x, &r));
+    return py::make_tuple(m, x, r);
+  }
   py::tuple profile_search(py::array_t<float, py::array::c_style | py::array::forcecast> q, uint32_t k,
                            uint32_t ef, int space) {
     const uint64_t nq = q.shape(0);
@@ -938,6 +960,9 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("last_counters", &PyIndexInterface::last_counters)
       .def("set_hash_log2", &PyIndexInterface::set_hash_log2)
       .def("set_visited_mode", &PyIndexInterface::set_visited_mode)
+      .def("set_helpers", &PyIndexInterface::set_helpers)
+      .def("last_launch", &PyIndexInterface::last_launch)
+      .def("help_stats", &PyIndexInterface::help_stats)
       .def("set_rerank_mode", &PyIndexInterface::set_rerank_mode)
       .def("rerank_mode", &PyIndexInterface::rerank_mode)
       .def("device_distances", &PyIndexInterface::device_distances)
@@ -964,6 +989,9 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("distances", &DeviceIndex::distances)
       .def("set_hash_log2", &DeviceIndex::set_hash_log2)
       .def("set_visited_mode", &DeviceIndex::set_visited_mode)
+      .def("set_helpers", &DeviceIndex::set_helpers)
+      .def("last_launch", &DeviceIndex::last_launch)
+      .def("help_stats", &DeviceIndex::help_stats)
       .def("flat_search", &DeviceIndex::flat_search, py::arg("queries"), py::arg("k"))
       .def("flat_search_device", &DeviceIndex::flat_search_device)
       .def("flat_diag", &DeviceIndex::flat_diag)
@@ -1000,4 +1028,11 @@ PYBIND11_MODULE(_alayalitepy, m) {
     check(alaya_hbm_stream_read(device, bytes, iters, &gbs));
     return gbs;
   }, py::arg("device") = 0, py::arg("bytes") = 4ull << 30, py::arg("iters") = 5);
+  // a CU-masked stream (handle as an int, for torch.cuda.ExternalStream) and its release
+  m.def("stream_create_reserving", [](int device, uint32_t reserved_cus) {
+    void *s = nullptr;
+    check(alaya_stream_create_reserving(device, reserved_cus, &s));
+    return reinterpret_cast<uintptr_t>(s);
+  }, py::arg("device"), py::arg("reserved_cus"));
+  m.def("stream_destroy", [](uintptr_t s) { check(alaya_stream_destroy(reinterpret_cast<void *>(s))); });
 }

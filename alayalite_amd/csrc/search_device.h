@@ -73,10 +73,14 @@ struct Lds {
 };
 
 // Distance of the query to candidate rows in the index's search space.
-template <bool kIP, int kChunks, int kSpace>
+// kSkip: the id list may hold kEmpty entries -- rows whose distance the caller already has (a helper's
+// memo, search kernel kMode 4); they take a row slot but load nothing new and write no output.
+// kRows: rows per lane group of an f32 row pass (0 = rows_per_group: the pass that fills one wave
+// per SIMD's registers; 1 = the two-waves-per-SIMD wide-row kernels, search kernel kMode 8).
+template <bool kIP, int kChunks, int kSpace, bool kSkip = false, int kRows = 0>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out);
-template <bool kIP, int kChunks, int kSpace, typename Hook>
+template <bool kIP, int kChunks, int kSpace, bool kSkip = false, int kRows = 0, typename Hook>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out, Hook after_issue);
 
@@ -133,38 +137,56 @@ __device__ __forceinline__ float finish_tail(const SearchParams &p, const float 
 #ifndef ALAYA_NARROW_RPL
 #define ALAYA_NARROW_RPL 2  // diagnostics builds: -DALAYA_NARROW_RPL=1 (8-row passes, fewer VGPRs)
 #endif
+#ifndef ALAYA_WIDE_RPL
+#define ALAYA_WIDE_RPL 0  // diagnostics builds: rows per lane group of the wide-row kernels (0 = 96 / chunks)
+#endif
 template <int kChunks>
 constexpr int rows_per_group() {
   return kChunks <= 0 ? 1
          : kChunks <= 8 ? ALAYA_NARROW_RPL
+         : ALAYA_WIDE_RPL > 0 ? ALAYA_WIDE_RPL
                         : (96 / kChunks >= 4 ? 4 : (96 / kChunks < 1 ? 1 : 96 / kChunks));
 }
 
 // One pass of row loads in registers: lane group g (8 lanes) takes rows base + g + 8r, r < kR.
-template <int kChunks>
+template <int kChunks, int kRows = 0>
 struct RowPass {
-  static constexpr int kR = rows_per_group<kChunks>();
+  static constexpr int kR = kRows > 0 ? kRows : rows_per_group<kChunks>();
   uint32_t id[kR];
   bool act[kR];
   float4 y[kR][kChunks];
 };
 
+// The row a lane group loads in place of a missing one (past n, or a kSkip kEmpty entry): the pass's
+// first id, or row 0 when that one is kEmpty too -- a load whose result is dropped.
+template <bool kSkip>
+__device__ __forceinline__ uint32_t stand_in_row(uint32_t first) {
+  if constexpr (kSkip) return first == kEmpty ? 0u : first;
+  return first;
+}
+
 // Issue every row chunk of the pass (all loads in flight before the first FMA).  Branch-free: a
 // lane group past n loads the pass's first row again (its result is dropped), and a whole slot
 // past n is skipped wave-uniformly -- per-load exec-mask branches would serialise the issue.
 // Requires base < n.
-template <int kChunks>
+template <int kChunks, bool kSkip = false, int kRows = 0>
 __device__ __forceinline__ void issue_rows(const SearchParams &p, const uint32_t *ids, int n, int base,
-                                           RowPass<kChunks> &P) {
-  constexpr int kRPL = RowPass<kChunks>::kR;
+                                           RowPass<kChunks, kRows> &P) {
+  constexpr int kRPL = RowPass<kChunks, kRows>::kR;
   const int lane = lane_id();
   const int g = lane >> 3, m = lane & 7;
-  const uint32_t id0 = ids[base];
+  const uint32_t id0 = stand_in_row<kSkip>(ids[base]);
 #pragma unroll
   for (int r = 0; r < kRPL; ++r) {
     const int idx = base + g + 8 * r;
-    P.act[r] = idx < n;
-    P.id[r] = P.act[r] ? ids[idx] : id0;
+    if constexpr (kSkip) {
+      const uint32_t id = idx < n ? ids[idx] : kEmpty;
+      P.act[r] = id != kEmpty;
+      P.id[r] = P.act[r] ? id : id0;
+    } else {
+      P.act[r] = idx < n;
+      P.id[r] = P.act[r] ? ids[idx] : id0;
+    }
   }
 #pragma unroll
   for (int r = 0; r < kRPL; ++r) {
@@ -179,10 +201,10 @@ __device__ __forceinline__ void issue_rows(const SearchParams &p, const uint32_t
 // Distances of an issued pass -> out[base + g + 8r].  The kChunks > 0 kernels run only for
 // dim == 32 * kChunks (search_kernel_symbol / the build's dispatch pick them from dim % 32 == 0), so
 // there is no 8-block or scalar tail.  Row slots past n (wave-uniform) are skipped whole.
-template <bool kIP, int kChunks>
+template <bool kIP, int kChunks, int kRows = 0>
 __device__ __forceinline__ void finish_rows(const SearchParams &p, const float *q, int n, int base,
-                                            RowPass<kChunks> &P, float *out) {
-  constexpr int kRPL = RowPass<kChunks>::kR;
+                                            RowPass<kChunks, kRows> &P, float *out) {
+  constexpr int kRPL = RowPass<kChunks, kRows>::kR;
   const int lane = lane_id();
   const int g = lane >> 3, m = lane & 7;
   int live = 0;  // wave-uniform number of row slots in use
@@ -220,7 +242,7 @@ __device__ __forceinline__ void finish_rows(const SearchParams &p, const float *
 // diff*diff (x*y) rounded before the add (-ffp-contract=off).  The reference builds it with -Ofast,
 // which leaves the order to the compiler; the source order is the restatement's (oracle generic_l2),
 // and every order agrees while the partial sums stay integers below 2^24.  One lane per row.
-template <bool kIP>
+template <bool kIP, bool kSkip = false>
 __device__ __forceinline__ void generic_distances(const SearchParams &p, const float *q,
                                                   const uint32_t *ids, int n, float *out) {
   const int lane = lane_id();
@@ -228,6 +250,7 @@ __device__ __forceinline__ void generic_distances(const SearchParams &p, const f
     const int r = base + lane;
     if (r < n) {
       const uint32_t id = ids[r];
+      if (kSkip && id == kEmpty) continue;  // known to the caller
       const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
       float sum = 0.f;
       for (uint32_t e = 0; e < p.dim; ++e) {
@@ -246,12 +269,12 @@ __device__ __forceinline__ void generic_distances(const SearchParams &p, const f
   wave_sync();
 }
 
-template <bool kIP, int kChunks>
+template <bool kIP, int kChunks, bool kSkip = false, int kRows = 0>
 __device__ __forceinline__ void row_distances(const SearchParams &p, const float *q,
                                               const uint32_t *ids, int n, float *out) {
   if constexpr (kChunks == 0) {
     if (p.generic) {  // wave-uniform; the host selects the kChunks == 0 kernels for generic rows
-      generic_distances<kIP>(p, q, ids, n, out);
+      generic_distances<kIP, kSkip>(p, q, ids, n, out);
       return;
     }
   }
@@ -262,18 +285,19 @@ __device__ __forceinline__ void row_distances(const SearchParams &p, const float
   const int nb8 = rem >> 3;
   const int tail_begin = 32 * T + 8 * nb8;
   if constexpr (kChunks > 0) {
-    constexpr int kStep = 8 * RowPass<kChunks>::kR;
+    constexpr int kStep = 8 * RowPass<kChunks, kRows>::kR;
     for (int base = 0; base < n; base += kStep) {
-      RowPass<kChunks> P;
-      issue_rows<kChunks>(p, ids, n, base, P);
-      finish_rows<kIP, kChunks>(p, q, n, base, P, out);
+      RowPass<kChunks, kRows> P;
+      issue_rows<kChunks, kSkip, kRows>(p, ids, n, base, P);
+      finish_rows<kIP, kChunks, kRows>(p, q, n, base, P, out);
     }
     (void)g; (void)m; (void)tail_begin;
   } else {
     for (int base = 0; base < n; base += 8) {
       const int r = base + g;
-      const bool act = r < n;
-      const uint32_t id = act ? ids[r] : 0u;
+      const uint32_t rid = r < n ? ids[r] : kEmpty;
+      const bool act = r < n && (!kSkip || rid != kEmpty);
+      const uint32_t id = act ? rid : 0u;
       const float *row = p.base + static_cast<uint64_t>(id) * p.stride;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
       if (act) {
@@ -358,19 +382,25 @@ struct Sq8Pass {
   uint32_t w[kR][kFull > 0 ? kFull : 1];
 };
 
-template <int kOrder, int kFull>
+template <int kOrder, int kFull, bool kSkip = false>
 __device__ __forceinline__ void sq8_issue(const SearchParams &p, const uint32_t *ids, int n, int base,
                                           Sq8Pass<kOrder, kFull> &S) {
   static_assert(kFull > 0, "compile-time chunk count only");
   using SP = Sq8Pass<kOrder, kFull>;
   const int lane = lane_id();
   const int g = lane / SP::LPR, m = lane % SP::LPR;
-  const uint32_t id0 = ids[base];
+  const uint32_t id0 = stand_in_row<kSkip>(ids[base]);
 #pragma unroll
   for (int r = 0; r < SP::kR; ++r) {
     const int idx = base + g + SP::G * r;
-    S.act[r] = idx < n;
-    S.id[r] = S.act[r] ? ids[idx] : id0;
+    if constexpr (kSkip) {
+      const uint32_t id = idx < n ? ids[idx] : kEmpty;
+      S.act[r] = id != kEmpty;
+      S.id[r] = S.act[r] ? id : id0;
+    } else {
+      S.act[r] = idx < n;
+      S.id[r] = S.act[r] ? ids[idx] : id0;
+    }
   }
 #pragma unroll
   for (int r = 0; r < SP::kR; ++r) {
@@ -464,7 +494,7 @@ struct NoHook {
 
 // after_issue() runs once, right after the first pass's row loads are issued (the search kernel
 // issues its second-level prefetch there, so it overlaps the rows' latency)
-template <bool kIP, int kOrder, int kFull, typename Hook = NoHook>
+template <bool kIP, int kOrder, int kFull, bool kSkip = false, typename Hook = NoHook>
 __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float *xq,
                                               const float *sc, const float *mnv,
                                               const uint32_t *ids, int n, float *out, Hook after_issue = Hook()) {
@@ -475,7 +505,7 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
   if constexpr (kFull > 0) {
     for (int base = 0; base < n; base += G * kRPL) {
       Sq8Pass<kOrder, kFull> S;
-      sq8_issue<kOrder, kFull>(p, ids, n, base, S);
+      sq8_issue<kOrder, kFull, kSkip>(p, ids, n, base, S);
       if (base == 0) after_issue();
       sq8_finish<kIP, kOrder, kFull>(p, xq, sc, mnv, n, base, S, out);
     }
@@ -497,8 +527,9 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
 #pragma unroll
     for (int r = 0; r < kRPL; ++r) {
       const int idx = base + g + G * r;
-      act[r] = idx < n;
-      id[r] = act[r] ? ids[idx] : 0u;
+      const uint32_t rid = idx < n ? ids[idx] : kEmpty;
+      act[r] = idx < n && (!kSkip || rid != kEmpty);
+      id[r] = act[r] ? rid : 0u;
       row[r] = p.codes + static_cast<uint64_t>(id[r]) * p.code_stride;
       acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0.f;
     }
@@ -550,22 +581,22 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
   wave_sync();
 }
 
-template <bool kIP, int kChunks, int kSpace, typename Hook>
+template <bool kIP, int kChunks, int kSpace, bool kSkip, int kRows, typename Hook>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out, Hook after_issue) {
   if constexpr (kSpace == 0) {
-    row_distances<kIP, kChunks>(p, L.q, ids, n, out);
+    row_distances<kIP, kChunks, kSkip, kRows>(p, L.q, ids, n, out);
     after_issue();
   } else {
-    sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks>(p, L.q, L.sq_scale, L.sq_min, ids, n, out,
-                                                                      after_issue);
+    sq8_distances<kIP, kSpace, kSpace == 2 ? kChunks : 2 * kChunks, kSkip>(p, L.q, L.sq_scale, L.sq_min, ids, n,
+                                                                             out, after_issue);
   }
 }
 
-template <bool kIP, int kChunks, int kSpace>
+template <bool kIP, int kChunks, int kSpace, bool kSkip, int kRows>
 __device__ __forceinline__ void space_distances(const SearchParams &p, const Lds &L,
                                                 const uint32_t *ids, int n, float *out) {
-  space_distances<kIP, kChunks, kSpace>(p, L, ids, n, out, NoHook());
+  space_distances<kIP, kChunks, kSpace, kSkip, kRows>(p, L, ids, n, out, NoHook());
 }
 
 // --------------------------------------------------------------------------------------------
@@ -735,16 +766,22 @@ __device__ __forceinline__ void stab_key(const Visited &vs, uint32_t v, uint32_t
   code = 1u + (h & ((1u << vs.stab_rbits) - 1u));
 }
 
+// Scope of every spill-table access (diagnostics builds: -DALAYA_STAB_SCOPE=__HIP_MEMORY_SCOPE_WORKGROUP
+// keeps the table's lines in the XCD's L2 -- a slot's table is only ever touched by the one wave that
+// owns the slot during a launch, and kernel boundaries order launches)
+#ifndef ALAYA_STAB_SCOPE
+#define ALAYA_STAB_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#endif
 __device__ __forceinline__ void stab_load(const Visited &vs, uint32_t bucket, uint64_t &lo, uint64_t &hi) {
   uint64_t *b = reinterpret_cast<uint64_t *>(vs.stab + static_cast<size_t>(bucket) * kStabBucket);
-  lo = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  hi = __hip_atomic_load(b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  lo = __hip_atomic_load(b, __ATOMIC_RELAXED, ALAYA_STAB_SCOPE);
+  hi = __hip_atomic_load(b + 1, __ATOMIC_RELAXED, ALAYA_STAB_SCOPE);
 }
 
 // Stores are agent-scope too: a plain (CU-scope) store may be acknowledged before it reaches L2, where
 // the wave's next agent-scope read of the bucket looks (measured: duplicate visits with plain stores).
 __device__ __forceinline__ void stab_store(const Visited &vs, uint32_t entry, uint32_t code) {
-  __hip_atomic_store(vs.stab + entry, static_cast<uint16_t>(code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(vs.stab + entry, static_cast<uint16_t>(code), __ATOMIC_RELAXED, ALAYA_STAB_SCOPE);
 }
 
 // Order the wave's earlier spill-table stores (and bitset atomics) before its later bucket reads.
@@ -946,7 +983,7 @@ __device__ __forceinline__ void visit_end(Visited &vs) {
   if (vs.stab != nullptr) {  // agent-scope stores: the next query's agent-scope reads see the zeros
     uint64_t *t = reinterpret_cast<uint64_t *>(vs.stab);
     const uint32_t n8 = 2u * (vs.stab_bmask + 1u);  // two 8-byte halves per bucket
-    for (uint32_t i = lane; i < n8; i += 64) __hip_atomic_store(t + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = lane; i < n8; i += 64) __hip_atomic_store(t + i, 0ull, __ATOMIC_RELAXED, ALAYA_STAB_SCOPE);
   }
   // agent-scope stores: the next query's atomics (performed in L2) must find them there
   if (vs.ndirty <= vs.dirty_cap) {
@@ -1111,19 +1148,31 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   if (first_pos < ps.cur) ps.cur = first_pos;
 }
 
-// LinearPool::pop: mark cur checked, advance to the next unchecked entry.
-__device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L) {
+// LinearPool::pop: mark cur checked, advance to the next unchecked entry.  kNext: also report the
+// ids of the first two unchecked entries after the pop (c1 = the new cur; c2 only from the same
+// 64-entry scan, else kEmpty) -- the distance helpers' requests.
+template <bool kNext = false>
+__device__ __forceinline__ uint32_t pool_pop(PoolState &ps, const Lds &L, uint32_t *c1 = nullptr,
+                                             uint32_t *c2 = nullptr) {
   const int lane = lane_id();
   const uint32_t raw = L.pi[ps.cur];
   wave_sync();
   if (lane == 0) L.pi[ps.cur] = raw | kChecked;
   uint32_t next = ps.size;
+  if constexpr (kNext) *c1 = *c2 = kEmpty;
   for (uint32_t b = ps.cur + 1; b < ps.size; b += 64) {
     const uint32_t j = b + lane;
-    const bool un = j < ps.size && !(L.pi[j] & kChecked);
+    const uint32_t pij = j < ps.size ? L.pi[j] : kChecked;
+    const bool un = !(pij & kChecked);
     const uint64_t mk = ballot(un);
     if (mk) {
-      next = b + __ffsll(static_cast<unsigned long long>(mk)) - 1;
+      const int f = __ffsll(static_cast<unsigned long long>(mk)) - 1;
+      next = b + f;
+      if constexpr (kNext) {
+        *c1 = read_lane(pij & kIdMask, f);
+        const uint64_t mk2 = mk & (mk - 1ull);
+        if (mk2) *c2 = read_lane(pij & kIdMask, __ffsll(static_cast<unsigned long long>(mk2)) - 1);
+      }
       break;
     }
   }

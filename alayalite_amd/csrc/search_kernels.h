@@ -71,6 +71,16 @@ struct SearchParams {
   uint32_t code_stride;
   const float *sq_min;    // per-dimension min / max of SQ8Quantizer (sq8.hpp:99-113)
   const float *sq_max;
+  // distance helpers (search_has_helpers): 1 = a wave with no query left computes its workgroup
+  // siblings' next distances into an LDS memo (kHelpBoardBytes after the wave regions); help_flags
+  // are diagnostics (ALAYA_HELP_FLAGS bit 0 = helpers compute every claimed row, no visited hint)
+  uint32_t help;
+  uint32_t help_flags;
+  uint32_t memo_off;      // byte offset of a helper's memo in its wave region (0: the query vector)
+  uint32_t two_waves;     // 1 = the wide-row f32 kernel at two waves per SIMD (one row per lane group):
+                          // twice the resident searchers, each with half the rows in flight
+  uint32_t *help_stats;   // nullable: per searcher, (fresh distances it took from a memo, expansions
+                          // with every fresh distance from the memo, rows it computed as a helper)
 };
 
 // PyIndex::rerank inputs (python/include/index.hpp:450-488).  Per query the kernel rescores
@@ -93,6 +103,11 @@ struct RerankParams {
 };
 
 constexpr uint32_t kVisWide = 0xffffffffu;
+constexpr size_t kHelpBoardBytes = 256;  // the helpers' request board (search kernel, kMode 4)
+#ifndef ALAYA_HELP_DEPTH
+#define ALAYA_HELP_DEPTH 1
+#endif
+constexpr size_t kHelpMemoSlots = ALAYA_HELP_DEPTH + 1;  // memo rows (requests) per searcher
 constexpr uint32_t kStabBucket = 8;  // spill-table entries per bucket (16 B: one prefetch per lane)
 // bytes of the LDS visited table / of one wave's LDS region / of a workgroup's shared region
 // (SQ8: the quantizer's per-dimension scale and min); a workgroup of W waves takes
@@ -107,6 +122,10 @@ __host__ __device__ inline size_t search_shared_lds_bytes(uint32_t stride, bool 
 // rerank: p.base/p.queries are the raw f32 rows and the (normalised) f32 queries
 hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream_t stream);
 hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu);
+// whether a search of this shape has a helper kernel (SearchParams::help)
+bool search_has_helpers(uint32_t dim, int sq8_order, bool generic);
+// whether a search of this shape has a two-waves-per-SIMD kernel (SearchParams::two_waves)
+bool search_has_two_waves(uint32_t dim, int sq8_order, bool generic);
 hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream);
 // out[q * n + i] = dist(queries[q], base[ids[i]]) for q < nq (bit-exact device distance)
 hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint32_t n,

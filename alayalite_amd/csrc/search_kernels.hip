@@ -36,6 +36,9 @@
 #ifndef ALAYA_MIN_WAVES_NARROW
 #define ALAYA_MIN_WAVES_NARROW 0
 #endif
+#ifndef ALAYA_MIN_WAVES_WIDE
+#define ALAYA_MIN_WAVES_WIDE 0  // diagnostics: waves per SIMD for the f32 kernels with d > 256
+#endif
 // kSpace: 0 = f32 rows, 1 = SQ8 codes in the AVX2 order, 2 = SQ8 codes in the AVX-512 order (the
 // kernels that run on the spill table).  f32 rows on the spill table were measured and dropped:
 // SIFT 1M at 10k queries 1.19 -> 1.47 ms, at 1k 0.55 -> 0.68 ms
@@ -45,13 +48,14 @@ constexpr bool space_sq8() { return kSpace == 1 || kSpace == 2; }
 template <int kSpace>
 constexpr bool space_tab() { return kSpace == 2; }
 
-template <int kChunks, int kSpace>
+template <int kChunks, int kSpace, int kMode = 0>
 constexpr int search_min_waves() {
+  if constexpr ((kMode & 8) != 0) return 2;  // the two-waves-per-SIMD wide-row kernels
   if constexpr (space_sq8<kSpace>()) {
     if (ALAYA_MIN_WAVES_SQ8 >= 0) return ALAYA_MIN_WAVES_SQ8;
     return kSpace == 2 && kChunks > 0 ? 4 : 0;
   }
-  return kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : 0;
+  return kChunks > 0 && kChunks <= 8 ? ALAYA_MIN_WAVES_NARROW : (kChunks > 8 ? ALAYA_MIN_WAVES_WIDE : 0);
 }
 
 namespace alaya_amd {
@@ -104,7 +108,7 @@ __device__ __forceinline__ void fill_shared(const SearchParams &p, const Lds &L)
 
 // Per-query setup shared by the search kernels: the query staged in LDS (SQ8: encoded with the
 // quantizer), visited table and pool cleared, then Graph::initialize_search (graph.hpp:148-158).
-template <bool kIP, int kChunks, int kSpace>
+template <bool kIP, int kChunks, int kSpace, int kRows = 0>
 __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L, uint32_t qi, uint32_t *slot_bits,
                                             uint32_t *slot_dirty, uint16_t *slot_stab, Visited &vs, PoolState &ps,
                                             uint32_t &n_dist_up, uint32_t &n_hops_up) {
@@ -156,7 +160,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
     uint64_t off_u = p.upper_off[u];  // u's upper-level lists, kept while u stays
     if (lane == 0) L.cid[0] = u;
     wave_sync();
-    space_distances<kIP, kChunks, kSpace>(p, L, L.cid, 1, L.cd);
+    space_distances<kIP, kChunks, kSpace, false, kRows>(p, L, L.cid, 1, L.cd);
     float cur = L.cd[0];
     ++n_dist_up;
     for (int level = static_cast<int>(p.levels[u]); level > 0; --level) {
@@ -177,7 +181,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
         wave_sync();
         if (has) L.cid[lane] = v;
         wave_sync();
-        space_distances<kIP, kChunks, kSpace>(p, L, L.cid, cnt, L.cd);
+        space_distances<kIP, kChunks, kSpace, false, kRows>(p, L, L.cid, cnt, L.cd);
         n_dist_up += cnt;
         // first index of the minimum == the sequential strict-'<' scan's final choice (the minimum
         // is order-free: DPP / swizzle steps within each 32-lane half, then the two halves)
@@ -219,7 +223,7 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
       if (has) L.cid[lane] = v;
       wave_sync();
       for (uint32_t c = 0; c < cnt; c += 8) {
-        space_distances<kIP, kChunks, kSpace>(p, L, L.cid + c, min(8u, cnt - c), L.cd + c);
+        space_distances<kIP, kChunks, kSpace, false, kRows>(p, L, L.cid + c, min(8u, cnt - c), L.cd + c);
       }
       n_dist_up += cnt;
       const float d = has ? L.cd[lane] : 0.f;
@@ -262,27 +266,328 @@ __device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, c
 }
 
 // --------------------------------------------------------------------------------------------
+// Distance helpers.  A searcher with no query left (the batch counter ran out) computes distances
+// for the siblings of its workgroup that are still searching.  Each searcher keeps three requests on
+// the workgroup's board: the node it is expanding (until it has read the memo) and the nodes it will
+// most likely expand next -- the pool's first two unchecked entries right after each pop, and the
+// merge's new next pop when it changes (the prediction holds ~99.8 % of the time for the next
+// expansion).  Helpers claim 16 adjacency
+// positions of a request at a time (older requests first: the nearer expansion), compute those
+// rows' distances against the sibling's query and store (request seq, distance) per position in
+// one memo, held in the region of the first wave that became a helper.  When the searcher expands
+// a requested node it takes the memo's distance for every fresh neighbour whose entry carries the
+// request's seq, and computes the rest itself -- none when the helpers kept up, so the expansion has
+// no row gather at all.  The distances are deterministic (same function, same query vector, same
+// row) and the searcher still does every visit, merge and pop itself, so ids, distances and
+// counters are those of the search without helpers; a helper that falls behind or answers a stale
+// request only costs work.  The reference keeps every worker busy to the end with its coroutine
+// interleave (include/executor/worker.hpp:47,111-136); here the batch tail's idle waves (and, in
+// batches smaller than the resident searchers, the spare ones) shorten the remaining searchers'
+// expansions instead.
+// LDS: a 208-byte board after the workgroup's wave regions; the memo (W x 3 x R entries of 8 bytes)
+// at byte p.memo_off of the memo wave's region -- its query vector or its pool and visited table,
+// unused once it has no query.
+// --------------------------------------------------------------------------------------------
+// How far ahead a searcher asks: 1 = the next expansion, 2 = the next two (diagnostics builds:
+// -DALAYA_HELP_DEPTH=2).  One slot more than the depth keeps the expanding node's request alive
+// until its memo entries are read.
+#ifndef ALAYA_HELP_DEPTH
+#define ALAYA_HELP_DEPTH 1
+#endif
+constexpr int kHelpDepth = ALAYA_HELP_DEPTH;
+static_assert(kHelpDepth == 1 || kHelpDepth == 2, "help depth 1 or 2");
+constexpr int kHelpSlots = kHelpDepth + 1;  // requests per searcher
+constexpr uint32_t kHelpClaim = 16;         // adjacency positions per claim (one row pass)
+struct HelpOwner {                          // one searcher's requests
+  uint64_t req[kHelpSlots];                 // (seq << 32) | node per slot; node kEmpty = none; seq only grows
+  uint32_t claim[kHelpSlots];               // (seq mod 2^24) << 8 | next adjacency position to hand out
+  uint32_t hits;                            // fresh distances taken from the memo (help_stats)
+  uint32_t skips;                           // expansions whose fresh distances all came from the memo
+  uint32_t rows;                            // as a helper: rows whose distances it computed
+};
+struct HelpBoard {
+  HelpOwner own[4];
+  uint32_t mask;  // bits 0-3: waves with no query left (helpers); bits 8-15: 1 + the memo wave
+  uint32_t pad[3];
+};
+static_assert(sizeof(HelpBoard) <= kHelpBoardBytes, "board size");
+
+__device__ __forceinline__ HelpBoard *help_board(const SearchParams &p, unsigned char *smem, int W) {
+  return reinterpret_cast<HelpBoard *>(smem + search_shared_lds_bytes(p.stride, p.sq8_order != 0) +
+                                       static_cast<size_t>(W) * p.wave_lds);
+}
+
+__device__ __forceinline__ void help_board_init(HelpBoard *b) {
+  for (int i = 0; i < 4; ++i) {
+    for (int s = 0; s < kHelpSlots; ++s) {
+      b->own[i].req[s] = static_cast<uint64_t>(kEmpty);
+      b->own[i].claim[s] = 0u;
+    }
+    b->own[i].hits = 0u;
+    b->own[i].skips = 0u;
+    b->own[i].rows = 0u;
+  }
+  b->mask = 0u;
+}
+
+__device__ __forceinline__ uint32_t help_word(HelpBoard *b) {
+  return read_lane(__hip_atomic_load(&b->mask, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+}
+
+// A searcher's requests as (node, seq) pairs (wave-uniform; each pair is one 8-byte LDS word)
+struct HelpReqs {
+  uint32_t node[kHelpSlots];
+  uint32_t seq[kHelpSlots];
+};
+__device__ __forceinline__ HelpReqs help_reqs(HelpBoard *b, int t) {
+  HelpReqs q;
+#pragma unroll
+  for (int s = 0; s < kHelpSlots; ++s) {
+    const uint64_t r = __hip_atomic_load(&b->own[t].req[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    q.node[s] = read_lane(static_cast<uint32_t>(r), 0);
+    q.seq[s] = read_lane(static_cast<uint32_t>(r >> 32), 0);
+  }
+  return q;
+}
+
+// A new query: no request of the previous one may match again (memo entries are tagged with a seq
+// that only grows; emptied slots are skipped by the helpers).
+__device__ __forceinline__ void help_reset(HelpBoard *b, int wave) {
+  if (lane_id() < kHelpSlots)
+    __hip_atomic_store(&b->own[wave].req[lane_id()], static_cast<uint64_t>(kEmpty), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The searcher has read the memo for slot s: no helper should start more work on that request.
+__device__ __forceinline__ void help_retire(HelpBoard *b, int wave, int s, uint32_t seq) {
+  if (lane_id() == 0)
+    __hip_atomic_store(&b->own[wave].claim[s], ((seq & 0xffffffu) << 8) | 0xffu, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The searcher's side of the board, kept in (scalar) registers so that an expansion pays no LDS
+// round trip for it: its requests, its seq counter and the memo wave (-1 while it has no helper).
+struct HelpMine {
+  uint32_t node[kHelpSlots];
+  uint32_t seq[kHelpSlots];
+  uint32_t next_seq;
+  int memo_wave;
+};
+
+// A new request for `node` in slot s (lane 0: the claim word first, then the request, so a helper
+// that sees the request finds its claim reset).
+__device__ __forceinline__ void mine_publish(HelpBoard *b, int wave, HelpMine &m, int s, uint32_t node) {
+  const uint32_t seq = ++m.next_seq;
+  m.node[s] = node;
+  m.seq[s] = seq;
+  if (lane_id() == 0) {
+    HelpOwner &o = b->own[wave];
+    // the LDS performs one wave's operations in order: a compiler barrier keeps the claim before the
+    // request without the release's wait for every outstanding LDS and scalar load
+    __hip_atomic_store(&o.claim[s], (seq & 0xffffffu) << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    __hip_atomic_store(&o.req[s], (static_cast<uint64_t>(seq) << 32) | node, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// Requests for the next expansions c1 (and, at depth 2, c2; kEmpty: none), keeping the slot of the
+// node being expanded (u) until its memo entries are read: slots holding u, c1 or c2 stay, the others
+// take the missing ones (with depth + 1 slots there is always room).
+__device__ __forceinline__ void mine_request(HelpBoard *b, int wave, HelpMine &m, uint32_t u, uint32_t c1,
+                                             uint32_t c2) {
+  if (kHelpDepth < 2) c2 = kEmpty;
+  bool need1 = c1 != kEmpty, need2 = c2 != kEmpty && c2 != c1;
+#pragma unroll
+  for (int s = 0; s < kHelpSlots; ++s) {
+    need1 = need1 && m.node[s] != c1;
+    need2 = need2 && m.node[s] != c2;
+  }
+  if (!need1 && !need2) return;
+#pragma unroll
+  for (int s = 0; s < kHelpSlots; ++s) {
+    const uint32_t x = m.node[s];
+    if (x != kEmpty && (x == u || x == c1 || x == c2)) continue;  // a slot to keep
+    if (need1) {
+      mine_publish(b, wave, m, s, c1);
+      need1 = false;
+    } else if (need2) {
+      mine_publish(b, wave, m, s, c2);
+      need2 = false;
+    }
+  }
+}
+
+__device__ __forceinline__ void mine_reset(HelpBoard *b, int wave, HelpMine &m) {
+#pragma unroll
+  for (int s = 0; s < kHelpSlots; ++s) m.node[s] = kEmpty;
+  help_reset(b, wave);
+}
+
+// The memo: W x 2 x R entries (seq << 32 | distance bits) at p.memo_off of the memo wave's region.
+template <int kSpace>
+__device__ __forceinline__ uint64_t *help_memo(const SearchParams &p, unsigned char *smem, int memo_wave) {
+  return reinterpret_cast<uint64_t *>(reinterpret_cast<unsigned char *>(carve_lds<kSpace>(p, smem, memo_wave).q) +
+                                      p.memo_off);
+}
+
+// Whether sibling t has probably visited v already (a hint: read while the sibling writes, so it may
+// be stale either way): its LDS first level, and -- SQ8 on the spill table -- its spill-table bucket.
+template <int kSpace>
+__device__ __forceinline__ bool sibling_visited(const SearchParams &p, const Lds &Lt, int t, uint32_t v, bool want) {
+  Visited vt = make_visited(p, Lt.hash, nullptr, nullptr, nullptr);
+  bool seen = want && table_lookup(vt, v);
+  if constexpr (space_tab<kSpace>()) {
+    if (p.spill_table != nullptr) {
+      const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + t;
+      vt.stab = p.spill_table + (slot << p.stab_log2);
+      vt.stab_bmask = (1u << (p.stab_log2 - 3)) - 1u;
+      uint32_t home, code;
+      stab_key(vt, v, home, code);
+      uint64_t lo = 0ull, hi = 0ull;
+      if (want && !seen) stab_load(vt, home, lo, hi);
+      bool found;
+      uint32_t occ;
+      stab_scan(lo, hi, code, found, occ);
+      seen = seen || (want && found);
+    }
+  }
+  return seen;
+}
+
+// A wave whose batch counter ran out helps its siblings until every wave of the workgroup has none
+// left (then all exit: no wave ever waits for another).
+template <bool kIP, int kChunks, int kSpace>
+__device__ void help_siblings(const SearchParams &p, unsigned char *smem, const Lds &L, HelpBoard *b, int wave,
+                              int W) {
+  const int lane = lane_id();
+  const uint32_t R = p.R;
+  const uint32_t full = (1u << W) - 1u;
+  // the visited hint (skip rows the sibling has already visited): by default where a stale read costs
+  // a global round trip less than the rows it saves -- SQ8 on the spill table (config 5, 1k queries:
+  // 3.47 ms with it, 3.62 without); the f32 rows of the SIFT shape are cheaper to compute than to
+  // filter (10k queries: 1.138 ms without, 1.153 with).  ALAYA_HELP_FLAGS bit 0 / 1 force it off / on.
+  const bool hint = (p.help_flags & 2u) || (space_sq8<kSpace>() && !(p.help_flags & 1u));
+  uint32_t *exhausted = reinterpret_cast<uint32_t *>(L.sd);  // per (sibling, slot): a request fully claimed
+  if (lane < 4 * kHelpSlots) exhausted[lane] = 0u;
+  // the first helper's region holds the memo: clear this wave's (seq 0 = no entry), then claim the role
+  {
+    uint64_t *mine = help_memo<kSpace>(p, smem, wave);
+    for (uint32_t e = lane; e < static_cast<uint32_t>(W) * kHelpSlots * R; e += 64)
+      __hip_atomic_store(mine + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  wave_sync();
+  if (lane == 0) {
+    uint32_t cur = __hip_atomic_load(&b->mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while ((cur >> 8) == 0u) {
+      const uint32_t want = cur | (static_cast<uint32_t>(wave + 1) << 8);
+      const uint32_t old = atomicCAS(&b->mask, cur, want);
+      if (old == cur) break;
+      cur = old;
+    }
+    __hip_atomic_fetch_or(&b->mask, 1u << wave, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  wave_sync();
+  int t = wave;
+  for (;;) {
+    const uint32_t hw = help_word(b);
+    const uint32_t mask = hw & 0xffu;
+    if (mask == full) break;  // every sibling is done
+    uint64_t *memo = help_memo<kSpace>(p, smem, static_cast<int>(hw >> 8) - 1);
+    do {
+      t = t + 1 == W ? 0 : t + 1;
+    } while ((mask >> t) & 1u);
+    const HelpReqs r = help_reqs(b, t);
+    // the oldest open request first (the nearest expansion)
+    uint32_t order = 0u;  // slot indices, 2 bits each, oldest first
+    if constexpr (kHelpSlots == 2) {
+      order = r.seq[1] < r.seq[0] ? (1u | (0u << 2)) : (0u | (1u << 2));
+    } else {
+      const uint32_t a = r.seq[0], b1 = r.seq[1], c = r.seq[kHelpSlots - 1];
+      const int s0 = (a <= b1 && a <= c) ? 0 : (b1 <= c ? 1 : 2);
+      const int sa = (s0 + 1) % 3, sb = (s0 + 2) % 3;
+      const bool swap = r.seq[sb] < r.seq[sa];
+      order = static_cast<uint32_t>(s0) | (static_cast<uint32_t>(swap ? sb : sa) << 2) |
+              (static_cast<uint32_t>(swap ? sa : sb) << 4);
+    }
+    bool worked = false;
+    for (int k = 0; k < kHelpSlots && !worked; ++k) {
+      const int s = static_cast<int>((order >> (2 * k)) & 3u);
+      const uint32_t node = r.node[s], seq = r.seq[s];
+      if (node == kEmpty || seq == 0u || exhausted[t * kHelpSlots + s] == seq) continue;
+      uint32_t old = 0u;
+      if (lane == 0) old = atomicAdd(&b->own[t].claim[s], kHelpClaim);
+      old = read_lane(old, 0);
+      if ((old >> 8) != (seq & 0xffffffu)) continue;  // replaced by a newer request meanwhile
+      const uint32_t pos = old & 0xffu;
+      const uint32_t v = lane < static_cast<int>(R) ? p.l0[static_cast<uint64_t>(node) * R + lane] : kEmpty;
+      const uint64_t endm = ballot(lane < static_cast<int>(R) && v == kEmpty);
+      const uint32_t cnt = endm ? static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(endm)) - 1) : R;
+      if (pos >= cnt) {
+        if (lane == 0) exhausted[t * kHelpSlots + s] = seq;
+        wave_sync();
+        continue;
+      }
+      worked = true;
+      const Lds Lt = carve_lds<kSpace>(p, smem, t);
+      bool want = static_cast<uint32_t>(lane) >= pos && static_cast<uint32_t>(lane) < min(pos + kHelpClaim, cnt);
+      if (hint) want = want && !sibling_visited<kSpace>(p, Lt, t, v, want);
+      const uint64_t wm = ballot(want);
+      const int n = __popcll(wm);
+      if (n == 0) continue;
+      const uint32_t slot = __popcll(wm & ((1ull << lane) - 1ull));
+      if (want) L.cid[slot] = v;
+      wave_sync();
+      space_distances<kIP, kChunks, kSpace>(p, Lt, L.cid, n, L.cd);
+      if (lane == 0) b->own[wave].rows += static_cast<uint32_t>(n);
+      if (want) {
+        const uint64_t e = (static_cast<uint64_t>(seq) << 32) | __float_as_uint(L.cd[slot]);
+        __hip_atomic_store(memo + (static_cast<uint32_t>(t) * kHelpSlots + s) * R + lane, e, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      wave_sync();
+    }
+    if (!worked) __builtin_amdgcn_s_sleep(4);  // ~256 cycles: polls stay off the searchers' LDS
+  }
+}
+
+// --------------------------------------------------------------------------------------------
 // The search kernel.
 // --------------------------------------------------------------------------------------------
-// kDiag: 0 = the search; 1 = diagnostic build that accumulates s_memtime cycles per phase into
-// p.stamps (nq x 8):
-// [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
+// kMode bits: 1 = diagnostic build that accumulates s_memtime cycles per phase into p.stamps
+// (nq x 8): [0] init + overlay descent, [1] pop, [2] adjacency load + visited set, [3] distances,
 // [4] merge, [5] expansions after the visited table spilled, [6] whole query, [7] prefetch hits;
 // 2 = the spill-table prefetch check (ALAYA_SPILL_FLAGS bit 8: every bucket read one expansion ahead
-// is compared with a re-read at its use, and a stale one marks the query's counters).
-// A workgroup holds blockDim.x / 64 waves (1 for f32 rows, up to 4 for SQ8, which share the
-// quantizer's scale / min); each wave is an independent persistent searcher with its own visited
-// spill slot.  After fill_shared the waves never synchronise again.
-template <bool kIP, int kChunks, int kDiag, int kSpace = 0>
+// is compared with a re-read at its use, and a stale one marks the query's counters);
+// 4 = distance helpers (SearchParams::help): a wave with no query left computes the distances of a
+// sibling's next expansion into a memo the sibling reads (help_siblings below);
+// 8 = two waves per SIMD for wide f32 rows (one row per lane group, SearchParams::two_waves).
+// A workgroup holds blockDim.x / 64 waves (1 for wide f32 rows; 4 for SQ8, which share the
+// quantizer's scale / min, and for searches with helpers); each wave is an independent persistent
+// searcher with its own visited spill slot.  After fill_shared the waves never wait on each other.
+template <bool kIP, int kChunks, int kMode, int kSpace = 0>
 __global__ void __launch_bounds__(256)
-    __attribute__((amdgpu_waves_per_eu(search_min_waves<kChunks, kSpace>() ? search_min_waves<kChunks, kSpace>() : 1,
+    __attribute__((amdgpu_waves_per_eu(search_min_waves<kChunks, kSpace, kMode>() ? search_min_waves<kChunks, kSpace, kMode>() : 1,
                                        8))) hnsw_search_kernel(SearchParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr bool kStamp = kDiag == 1;
+  constexpr bool kStamp = (kMode & 1) != 0;
+  constexpr bool kCheck = (kMode & 2) != 0;
+  constexpr bool kHelp = (kMode & 4) != 0;
+  constexpr int kRows = (kMode & 8) != 0 ? 1 : 0;
   const int lane = lane_id();
   const int wave = static_cast<int>(threadIdx.x >> 6);
+  const int W = static_cast<int>(blockDim.x >> 6);
   const Lds L = carve_lds<kSpace>(p, smem, wave);
   fill_shared<kSpace>(p, L);
+  HelpBoard *board = kHelp ? help_board(p, smem, W) : nullptr;
+  HelpMine mine;
+  if constexpr (kHelp) {
+    if (threadIdx.x == 0) help_board_init(board);
+    __syncthreads();
+    for (int s = 0; s < kHelpSlots; ++s) mine.node[s] = kEmpty, mine.seq[s] = 0u;
+    mine.next_seq = 0u;
+    mine.memo_wave = -1;
+  }
   const uint64_t bit_words = (p.n + 31) / 32;
   const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
   uint32_t *slot_bits = p.overflow_bits + slot * bit_words;
@@ -291,11 +596,22 @@ __global__ void __launch_bounds__(256)
   // kernels carry none of it)
   uint16_t *slot_stab = (space_tab<kSpace>() && p.spill_table) ? p.spill_table + (slot << p.stab_log2) : nullptr;
 
+  bool first_round = true;
   for (;;) {
     uint32_t qi = 0;
-    if (lane == 0) qi = atomicAdd(p.work_counter, 1u);
-    qi = read_lane(qi, 0);
+    if (kHelp && first_round) {
+      // first round assigned wave-major over the workgroups, so a batch smaller than the resident
+      // searchers leaves every workgroup a mix of searchers and helpers; then the work counter
+      qi = static_cast<uint32_t>(wave) * gridDim.x + blockIdx.x;
+    } else {
+      if (lane == 0) qi = atomicAdd(p.work_counter, 1u);
+      qi = read_lane(qi, 0) + (kHelp ? static_cast<uint32_t>(W) * gridDim.x : 0u);
+    }
+    first_round = false;
     if (qi >= p.nq) break;
+    // a memo entry belongs to the query it was requested in: requests of an earlier query never
+    // match again (the seq only grows, and the requests are dropped here)
+    if constexpr (kHelp) mine_reset(board, wave, mine);
 
     uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t t_prev = kStamp ? __builtin_readcyclecounter() : 0;
@@ -310,7 +626,7 @@ __global__ void __launch_bounds__(256)
     Visited vs;
     PoolState ps;
     uint32_t n_dist = 0, n_expand = 0, n_dist_up = 0, n_hops_up = 0;
-    query_begin<kIP, kChunks, kSpace>(p, L, qi, slot_bits, slot_dirty, slot_stab, vs, ps, n_dist_up, n_hops_up);
+    query_begin<kIP, kChunks, kSpace, kRows>(p, L, qi, slot_bits, slot_dirty, slot_stab, vs, ps, n_dist_up, n_hops_up);
 
     // ---- best-first expansion (graph_search_job.hpp:228-252 / 310-330) -----------------------
     stamp(0);
@@ -331,8 +647,24 @@ __global__ void __launch_bounds__(256)
     uint32_t pre_u = kEmpty;
     uint64_t pre_lo = 0ull, pre_hi = 0ull;
     while (ps.cur < ps.size) {
-      const uint32_t u = pool_pop(ps, L);
+      uint32_t c1 = kEmpty, c2 = kEmpty;
+      const uint32_t u = pool_pop<kHelp>(ps, L, &c1, &c2);
       ++n_expand;
+      // helpers present: the request for this node (if any; its memo is read in the distance phase)
+      // and requests for the next two expansions as the pool stands now
+      uint32_t look = 0u;  // (seq << 2) | slot
+      if constexpr (kHelp) {
+        if (mine.memo_wave < 0 && (n_expand & 3u) == 1u) {  // (a helper appears at most once)
+          const uint32_t hw = help_word(board);
+          if ((hw >> 8) != 0u) mine.memo_wave = static_cast<int>(hw >> 8) - 1;
+        }
+        if (mine.memo_wave >= 0) {
+#pragma unroll
+          for (int hs = 0; hs < kHelpSlots; ++hs)
+            if (mine.node[hs] == u) look = (mine.seq[hs] << 2) | static_cast<uint32_t>(hs);
+          mine_request(board, wave, mine, u, c1, c2);
+        }
+      }
 #ifndef ALAYA_FINE_STAMPS
       if (kStamp && vs.spilled) st[5]++;
 #endif
@@ -359,7 +691,7 @@ __global__ void __launch_bounds__(256)
         }
       }
       if (!vs.spilled && vs.count + 64 > vs.limit) spill_begin<space_tab<kSpace>()>(vs);
-      if constexpr (kDiag == 2 && space_tab<kSpace>()) {
+      if constexpr (kCheck && space_tab<kSpace>()) {
         // diagnostics (tests/test_sq8_spill.py): the buckets read one expansion ahead must equal the
         // table as it is now; a stale one marks the query's counters
         if (u == pre_u && vs.spilled && vs.stab != nullptr) {
@@ -400,6 +732,35 @@ __global__ void __launch_bounds__(256)
       // compact fresh ids in adjacency order
       const uint32_t slot = __popcll(fm & ((1ull << lane) - 1ull));
       if (fresh) L.cid[slot] = v;
+      // distances a helper already computed for this node's row (exact: the same function of the same
+      // query and row) go straight to cd; the rest are computed here, the known ones standing in the
+      // list as kEmpty (distance functions skip them)
+      const uint32_t *dist_ids = L.cid;
+      bool compute = true;
+      if constexpr (kHelp) {
+        if (look != 0u) {
+          const uint32_t seq = look >> 2;
+          const int hs = static_cast<int>(look & 3u);
+          const uint64_t *memo = help_memo<kSpace>(p, smem, mine.memo_wave) +
+                                 (static_cast<uint32_t>(wave) * kHelpSlots + hs) * p.R;
+          uint64_t e = 0ull;
+          if (fresh) e = __hip_atomic_load(memo + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const bool got = fresh && static_cast<uint32_t>(e >> 32) == seq;
+          help_retire(board, wave, hs, seq);
+          uint32_t *ids2 = reinterpret_cast<uint32_t *>(L.sd);  // free until the merge
+          if (fresh) {
+            ids2[slot] = got ? kEmpty : v;
+            if (got) L.cd[slot] = __uint_as_float(static_cast<uint32_t>(e));
+          }
+          dist_ids = ids2;
+          const uint32_t n_got = __popcll(ballot(got));
+          if (lane == 0 && n_got) {
+            board->own[wave].hits += n_got;
+            if (n_got == static_cast<uint32_t>(nf)) board->own[wave].skips += 1u;
+          }
+          compute = n_got < static_cast<uint32_t>(nf);
+        }
+      }
       wave_sync();
       // The second-level prefetch of the predicted next expansion goes out right after this
       // expansion's first row pass is issued, so its latency overlaps the rows'.  It needs pred_v,
@@ -407,7 +768,7 @@ __global__ void __launch_bounds__(256)
       // that order) and before the rows: the wait for pred_v (vmcnt counts loads, stores and atomics
       // in issue order) is the wait for them too, so the prefetch reads the table as this visit left
       // it (ALAYA_SPILL_FLAGS bit 8 checks every prefetched bucket against a re-read).
-      space_distances<kIP, kChunks, kSpace>(p, L, L.cid, nf, L.cd, [&]() {
+      auto second_level_prefetch = [&]() {
         if constexpr (kSpillPrefetch) {
           if (vs.spilled && pred != kEmpty && !(p.spill_flags & 1u)) {
             if (p.spill_flags & 4u) __builtin_amdgcn_s_waitcnt(0);  // diagnostics: also wait for the rows
@@ -415,7 +776,12 @@ __global__ void __launch_bounds__(256)
             pre_u = pred;
           }
         }
-      });
+      };
+      if (!kHelp || compute) {
+        space_distances<kIP, kChunks, kSpace, kHelp, kRows>(p, L, dist_ids, nf, L.cd, second_level_prefetch);
+      } else {
+        second_level_prefetch();
+      }
       stamp(3);
       n_dist += nf;
       const bool has = lane < nf;
@@ -426,8 +792,13 @@ __global__ void __launch_bounds__(256)
       // rest of the merge and the pop run (the prediction above is then stale)
       pool_merge<kRegMerge>(ps, L, has, cid, cd, [&](uint32_t nx) {
         if (nx != pred) {
+          const uint32_t old_pred = pred;
+          (void)old_pred;
           pred = nx;
           if (lane < static_cast<int>(p.R)) pred_v = p.l0[static_cast<uint64_t>(nx) * p.R + lane];
+          if constexpr (kHelp) {  // the new next pop, keeping the old one's request (likely the one after)
+            if (mine.memo_wave >= 0) mine_request(board, wave, mine, kEmpty, nx, old_pred);
+          }
         }
       }
 #ifdef ALAYA_FINE_STAMPS
@@ -444,6 +815,14 @@ __global__ void __launch_bounds__(256)
       if (lane < 8) p.stamps[static_cast<uint64_t>(qi) * 8 + lane] = st[lane & 7];
     }
     wave_sync();
+  }
+  if constexpr (kHelp) {
+    help_siblings<kIP, kChunks, kSpace>(p, smem, L, board, wave, W);
+    if (p.help_stats != nullptr && lane == 0) {  // (the board outlives every wave's searching)
+      p.help_stats[3 * slot] = board->own[wave].hits;
+      p.help_stats[3 * slot + 1] = board->own[wave].skips;
+      p.help_stats[3 * slot + 2] = board->own[wave].rows;
+    }
   }
 }
 
@@ -599,18 +978,24 @@ hipError_t launch_rerank(const SearchParams &p, const RerankParams &r, hipStream
   return hipGetLastError();
 }
 
-template <bool kIP, int kChunks, int kDiag = 0, int kSpace = 0>
+template <bool kIP, int kChunks, int kMode = 0, int kSpace = 0>
 static const void *kernel_ptr() {
-  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kDiag, kSpace>);
+  return reinterpret_cast<const void *>(&hnsw_search_kernel<kIP, kChunks, kMode, kSpace>);
 }
 
 template <int kSpace>
-static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped, bool check) {
+static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped, bool check, bool help) {
   const uint32_t chunks = (dim % 32 == 0) ? dim / 32 : 0;
+  if constexpr (kSpace == 2) {  // stamped with helpers (tools/profile_phases.py)
+    if (stamped && help && chunks == 24) return ip ? kernel_ptr<true, 24, 5, kSpace>() : kernel_ptr<false, 24, 5, kSpace>();
+  }
   if (stamped && chunks == 24) return ip ? kernel_ptr<true, 24, 1, kSpace>() : kernel_ptr<false, 24, 1, kSpace>();
   if constexpr (kSpace == 2) {  // the spill-table prefetch check (config 5's d = 768 and d = 960)
     if (check && chunks == 24) return ip ? kernel_ptr<true, 24, 2, kSpace>() : kernel_ptr<false, 24, 2, kSpace>();
     if (check && chunks == 30) return ip ? kernel_ptr<true, 30, 2, kSpace>() : kernel_ptr<false, 30, 2, kSpace>();
+    if (help && chunks == 4) return ip ? kernel_ptr<true, 4, 4, kSpace>() : kernel_ptr<false, 4, 4, kSpace>();
+    if (help && chunks == 24) return ip ? kernel_ptr<true, 24, 4, kSpace>() : kernel_ptr<false, 24, 4, kSpace>();
+    if (help && chunks == 30) return ip ? kernel_ptr<true, 30, 4, kSpace>() : kernel_ptr<false, 30, 4, kSpace>();
   }
   if (chunks == 4) return ip ? kernel_ptr<true, 4, 0, kSpace>() : kernel_ptr<false, 4, 0, kSpace>();
   if (chunks == 24) return ip ? kernel_ptr<true, 24, 0, kSpace>() : kernel_ptr<false, 24, 0, kSpace>();
@@ -618,15 +1003,36 @@ static const void *sq8_symbol(bool ip, uint32_t dim, bool stamped, bool check) {
   return ip ? kernel_ptr<true, 0, 0, kSpace>() : kernel_ptr<false, 0, 0, kSpace>();
 }
 
-const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic, bool check) {
-  if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped, check);
-  if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped, false);
+// Whether a search has a helper kernel (kMode 4): the small-row f32 kernels (d = 128 / 256, the
+// latency-bound SIFT shape) and the AVX-512-order SQ8 kernels with a compile-time chunk count.  The
+// wide f32 rows (GIST, the headline) are bandwidth-bound: helpers would add bytes, not overlap.
+bool search_has_two_waves(uint32_t dim, int sq8_order, bool generic) {
+  return sq8_order == 0 && !generic && (dim == 24 * 32 || dim == 30 * 32);
+}
+
+bool search_has_helpers(uint32_t dim, int sq8_order, bool generic) {
+  if (generic || dim % 32 != 0) return false;
+  const uint32_t chunks = dim / 32;
+  if (sq8_order == 2) return chunks == 4 || chunks == 24 || chunks == 30;
+  if (sq8_order == 1) return false;
+  return chunks == 4 || chunks == 8;
+}
+
+const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_order, bool generic, bool check,
+                                 bool help, bool two_waves) {
+  if (sq8_order == 2) return sq8_symbol<2>(ip, dim, stamped, check, help);
+  if (sq8_order == 1) return sq8_symbol<1>(ip, dim, stamped, false, false);
   const uint32_t chunks = (!generic && dim % 32 == 0) ? dim / 32 : 0;  // generic order: the runtime-d kernel
   if (stamped) {
+    if (help && chunks == 4) return ip ? kernel_ptr<true, 4, 5>() : kernel_ptr<false, 4, 5>();
     if (chunks == 30) return ip ? kernel_ptr<true, 30, 1>() : kernel_ptr<false, 30, 1>();
     if (chunks == 4) return ip ? kernel_ptr<true, 4, 1>() : kernel_ptr<false, 4, 1>();
     return ip ? kernel_ptr<true, 0, 1>() : kernel_ptr<false, 0, 1>();
   }
+  if (help && chunks == 4) return ip ? kernel_ptr<true, 4, 4>() : kernel_ptr<false, 4, 4>();
+  if (help && chunks == 8) return ip ? kernel_ptr<true, 8, 4>() : kernel_ptr<false, 8, 4>();
+  if (two_waves && chunks == 24) return ip ? kernel_ptr<true, 24, 8>() : kernel_ptr<false, 24, 8>();
+  if (two_waves && chunks == 30) return ip ? kernel_ptr<true, 30, 8>() : kernel_ptr<false, 30, 8>();
 #define ALAYA_CASE(C)                                                        \
   if (chunks == C) return ip ? kernel_ptr<true, C>() : kernel_ptr<false, C>();
   ALAYA_CASE(4)
@@ -641,7 +1047,7 @@ const void *search_kernel_symbol(bool ip, uint32_t dim, bool stamped, int sq8_or
 
 hipError_t launch_search(const SearchParams &p, int grid, int waves, size_t lds, hipStream_t stream) {
   const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic,
-                                        (p.spill_flags & 256u) != 0);
+                                        (p.spill_flags & 256u) != 0, p.help != 0, p.two_waves != 0);
   SearchParams arg = p;
   void *args[] = {&arg};
   return hipLaunchKernel(fn, dim3(grid), dim3(64 * waves), args, lds, stream);
@@ -661,7 +1067,7 @@ hipError_t launch_row_distances(const SearchParams &p, const uint32_t *ids, uint
 
 hipError_t search_occupancy(const SearchParams &p, int waves, size_t lds, int *blocks_per_cu) {
   const void *fn = search_kernel_symbol(p.ip, p.dim, p.stamps != nullptr, p.sq8_order, p.generic,
-                                        (p.spill_flags & 256u) != 0);
+                                        (p.spill_flags & 256u) != 0, p.help != 0, p.two_waves != 0);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * waves, lds);
 }
 

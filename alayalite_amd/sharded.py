@@ -176,9 +176,15 @@ class ShardPipeline:
     device search.  On CPU tensors (gloo tests) the same loop runs without streams.
 
     search_fn(q, ids, dists, counters, stream_handle) launches one shard search (shard_search);
-    batches hold at most nq queries each."""
+    batches hold at most nq queries each.
 
-    def __init__(self, search_fn, nq: int, k: int, offset: int, device, group=None, timing: bool = False):
+    reserve_cus > 0 runs the compute stream on a CU-masked stream that leaves that many CUs to other
+    streams (alaya_stream_create_reserving): the search sizes its persistent grid to the CUs left,
+    so the exchange's kernels (RCCL's all_gather and the merge sort) start at once instead of
+    queueing behind the next batch's search."""
+
+    def __init__(self, search_fn, nq: int, k: int, offset: int, device, group=None, timing: bool = False,
+                 reserve_cus: int = 0):
         import torch
 
         self.search_fn, self.k, self.offset, self.group = search_fn, k, offset, group
@@ -188,8 +194,15 @@ class ShardPipeline:
         self.rows = [0, 0]
         self.packed = [None, None]  # packed keys of the batch in each slot (compute stream)
         self.gpu = self.device.type == "cuda"
+        self._masked = None
         if self.gpu:
-            self.compute = torch.cuda.Stream(self.device)
+            if reserve_cus > 0:
+                from ._native import _ext
+
+                self._masked = _ext.stream_create_reserving(self.device.index or 0, int(reserve_cus))
+                self.compute = torch.cuda.ExternalStream(self._masked, device=self.device)
+            else:
+                self.compute = torch.cuda.Stream(self.device)
             self.exch = torch.cuda.Stream(self.device)
             self.searched = [torch.cuda.Event() for _ in range(2)]
         self.timing = timing and self.gpu
@@ -257,6 +270,17 @@ class ShardPipeline:
                 d.record_stream(cur)
         return out
 
+    def close(self):
+        """Release the CU-masked compute stream (after the pipeline's work is done)."""
+        if self._masked is not None:
+            import torch
+
+            from ._native import _ext
+
+            torch.cuda.synchronize(self.device)
+            _ext.stream_destroy(self._masked)
+            self._masked = None
+
     def search_ms(self):
         """Mean search time (ms) of the batches run with timing=True, as the compute stream saw it
         inside the pipeline (after synchronisation)."""
@@ -315,10 +339,10 @@ class ShardedIndex:
         self.search_device(q_dev, k, ef, ids, d, c, stream)
         return exchange_and_merge(ids, d, self.lo, k, group)
 
-    def pipeline(self, nq: int, k: int, ef: int, group=None) -> ShardPipeline:
+    def pipeline(self, nq: int, k: int, ef: int, group=None, reserve_cus: int = 0) -> ShardPipeline:
         """A double-buffered pipeline for batches of nq queries at this ef (ShardPipeline)."""
         fn = lambda q, ids, d, c, s: self.search_device(q, k, ef, ids, d, c, s)  # noqa: E731
-        return ShardPipeline(fn, nq, k, self.lo, self.index_device(), group)
+        return ShardPipeline(fn, nq, k, self.lo, self.index_device(), group, reserve_cus=reserve_cus)
 
     def index_device(self):
         import torch

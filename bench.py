@@ -103,6 +103,9 @@ def parse():
                    help="N>1 shard mode: other S to measure beside the result: 'auto' (every divisor of N), "
                         "'none', or a comma list")
     p.add_argument("--no-replica-leg", action="store_true", help="alias of --layouts none")
+    p.add_argument("--exchange-cus", type=int, default=-1,
+                   help="CUs the pipelined shard search leaves to the exchange stream (CU-masked compute "
+                        "stream); -1 = 8 on the RCCL backend with N > 1, else 0")
     p.add_argument("--build-threads", type=int, default=0)
     p.add_argument("--builder", choices=("auto", "host", "gpu"), default="auto",
                    help="graph builder: host = HNSWBuilder restated on the host (cached; multi-threaded, so "
@@ -675,14 +678,16 @@ def main():
         # all_gather + merge of step i on a second stream); this is `value`, the synchronous loop
         # above (search, then exchange, per step) is reported beside it with the exchange alone
         sync_elapsed = elapsed
+        reserve = args.exchange_cus if args.exchange_cus >= 0 else (
+            8 if (world > 1 and dist.get_backend() == "nccl") else 0)
         elapsed, pipe_search_ms = timed_pipeline(torch, dist, dev, ef, args.steps, args.warmup, index, lo, use_sq8,
-                                                 q_dev, nq, group)
+                                                 q_dev, nq, group, reserve)
         exch_ms = timed_exchange(torch, dist, ids_dev, dists_dev, lo, args.steps, group)
         overlap = {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
                    "sync_ms_per_step": round(sync_elapsed / args.steps * 1e3, 4),
                    "search_ms": round(kernel_ms, 4), "search_ms_in_pipeline": round(pipe_search_ms, 4),
                    "exchange_ms": round(exch_ms, 4),
-                   "bound_ms": round(max(pipe_search_ms, exch_ms), 4),
+                   "bound_ms": round(max(pipe_search_ms, exch_ms), 4), "reserved_cus": reserve,
                    "note": "value = the overlapped steps; sync = search then exchange in one stream per step"}
         log("overlap", overlap)
 
@@ -859,14 +864,15 @@ def main():
         dist.destroy_process_group()
 
 
-def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_dev, nq, group=None):
+def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_dev, nq, group=None, reserve=0):
     """K shard steps through ShardPipeline (double-buffered: the search of step i+1 overlaps the
-    exchange of step i); barrier + synchronize on both sides, max over ranks.  Returns (seconds,
-    mean search ms inside the pipeline, from a second untimed pass with events)."""
+    exchange of step i; `reserve` CUs left to the exchange stream); barrier + synchronize on both
+    sides, max over ranks.  Returns (seconds, mean search ms inside the pipeline, from a second
+    untimed pass with events)."""
     from alayalite_amd.sharded import ShardPipeline, shard_search
 
     fn = lambda q, i, d, c, s: shard_search(index, lo, use_sq8, q, K, ef, i, d, c, s)  # noqa: E731
-    pipe = ShardPipeline(fn, nq, K, lo, dev, group)
+    pipe = ShardPipeline(fn, nq, K, lo, dev, group, reserve_cus=reserve)
     pipe.run([q_dev] * max(1, warmup))
     torch.cuda.synchronize()
     dist.barrier()
@@ -878,9 +884,11 @@ def timed_pipeline(torch, dist, dev, ef, steps, warmup, index, lo, use_sq8, q_de
     el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # the search time as it runs inside the pipeline (a separate, untimed pass with events)
-    tp = ShardPipeline(fn, nq, K, lo, dev, group, timing=True)
+    tp = ShardPipeline(fn, nq, K, lo, dev, group, timing=True, reserve_cus=reserve)
     tp.run([q_dev] * steps)
     torch.cuda.synchronize()
+    pipe.close()
+    tp.close()
     sm = torch.tensor([tp.search_ms()], device=dev, dtype=torch.float64)
     dist.all_reduce(sm, op=dist.ReduceOp.MAX)
     return el.item(), sm.item()

@@ -66,6 +66,12 @@ int alaya_device_count(int *count);
  * `bytes`-byte device buffer (>= 1 MiB) over three load shapes and two occupancies, in GB/s -- the
  * measured bandwidth ceiling bench.py reports beside the 8 TB/s HBM3E figure. */
 int alaya_hbm_stream_read(int device, uint64_t bytes, int iters, double *gbs);
+/* A HIP stream whose launches may use every CU of `device` but `reserved_cus` (spread over the CU
+ * numbering), so kernels of other streams -- the shard exchange's RCCL all_gather -- find free CUs
+ * while a persistent search runs; searches launched on it size their grid to the CUs left.  No
+ * reference counterpart (the reference is single-process CPU code). */
+int alaya_stream_create_reserving(int device, uint32_t reserved_cus, void **stream);
+int alaya_stream_destroy(void *stream);
 
 /* ---- host graph (builder + reference on-disk format) --------------------------------------- */
 /* data: n x dim float32 row-major (normalised already for COS).  seed 100 = reference default. */
@@ -221,6 +227,21 @@ int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint
  * the visited set is exact (DynamicBitset, include/utils/query_utils.hpp:69-115). */
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots);
 int alaya_index_set_visited_mode(alaya_index *ix, int mode);
+/* Distance helpers (-1 automatic, 0 off, 1 on; environment ALAYA_HELPERS overrides): a searcher
+ * whose batch has no query left computes the distances of a sibling searcher's predicted next
+ * expansion (same workgroup) into an LDS memo the sibling reads.  Replaces nothing in the reference:
+ * its coroutine scheduler keeps every worker busy to the end of a batch
+ * (include/executor/worker.hpp:47,111-136); results never depend on it (the searcher still does
+ * every visit, merge and pop; memo distances are the same function of the same inputs).
+ * alaya_index_help_stats: of the last search with helpers, how many of its fresh distances
+ * (the n_dist counters) the searchers took from a memo, in how many expansions every fresh distance
+ * came from it, and how many rows the helpers computed (waits for that search; 0 without helpers). */
+int alaya_index_set_helpers(alaya_index *ix, int mode);
+int alaya_index_help_stats(alaya_index *ix, uint64_t *memo_dists, uint64_t *memo_expansions,
+                           uint64_t *helper_rows);
+/* The last graph search's launch shape: persistent workgroups and searchers (waves) per workgroup --
+ * workgroups x waves is the number of queries the launch runs at once (introspection). */
+int alaya_index_last_launch(const alaya_index *ix, uint32_t *workgroups, uint32_t *waves_per_group);
 int alaya_index_info(const alaya_index *ix, uint64_t *n, uint32_t *dim, uint32_t *stride,
                      int *metric, uint64_t *device_bytes);
 

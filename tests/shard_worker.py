@@ -79,8 +79,12 @@ def main():
     # the same queries in three batches through the double-buffered pipeline
     cuts = [0, nq // 3, 2 * nq // 3, nq]
     batches = [q_dev[cuts[i]:cuts[i + 1]].contiguous() for i in range(3)]
-    res = shard.pipeline(max(b.shape[0] for b in batches), k, ef).run(batches)
+    # ALAYA_TEST_RESERVE_CUS: the pipeline's search on a CU-masked stream that leaves CUs to the exchange
+    pipe = shard.pipeline(max(b.shape[0] for b in batches), k, ef,
+                          reserve_cus=int(os.environ.get("ALAYA_TEST_RESERVE_CUS", "0")))
+    res = pipe.run(batches)
     torch.cuda.synchronize()
+    pipe.close()
     pipe_ids = [r[0].cpu().numpy() for r in res]
     pipe_d = [r[1].cpu().numpy() for r in res]
 

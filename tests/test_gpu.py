@@ -140,6 +140,21 @@ def test_search_gist_shaped(native, orc):
     _check(view, _dev(native, base, g), queries, 10, 80)
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("dim", [768, 960])
+def test_two_waves_per_simd_wide_rows(native, orc, monkeypatch, dim, metric):
+    """The wide-row f32 kernels at two waves per SIMD (one row per lane group, kMode 8), which a
+    batch just past the one-wave kernel's resident searchers runs (config 4's S = 1 layout), forced
+    here with ALAYA_TWO_WAVES=1: the same ids, distance bits and counters as the restatement."""
+    monkeypatch.setenv("ALAYA_TWO_WAVES", "1")
+    rng = np.random.default_rng(dim + metric)
+    centres = rng.uniform(0, 0.5, (16, dim)).astype(np.float32)
+    base = np.clip(centres[rng.integers(0, 16, 5000)] + rng.normal(0, 0.05, (5000, dim)), 0, 1).astype(np.float32)
+    queries = np.clip(centres[rng.integers(0, 16, 40)] + rng.normal(0, 0.05, (40, dim)), 0, 1).astype(np.float32)
+    g, view = _graph_view(native, orc, base, metric=metric, threads=8)
+    _check(view, _dev(native, base, g, metric), queries, 10, 96)
+
+
 def test_search_sift_shaped_many_queries(native, orc):
     rng = np.random.default_rng(4)
     base = rng.integers(0, 128, (20000, 128)).astype(np.float32)

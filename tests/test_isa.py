@@ -44,9 +44,9 @@ def test_fixed_d_f32_expansion_loops_restore_no_spilled_sgpr(census, metric, chu
 # The AVX-512-order SQ8 kernels carry the spill table (round 4: flush, bucket prefetch, bitset third
 # level), whose uniform state costs SGPR restores per expansion -- 12-31 v_readlane against ~12k
 # cycles per expansion at config 5 (measured on this image's hipcc: 12 in config 5's 768-d IP
-# kernel, 31 in the others).  The AVX2-order kernels keep the bitset (0-4 restores).  Budgets are
+# kernel, 31 in the others).  The AVX2-order kernels keep the bitset (0-6 restores).  Budgets are
 # the measured maxima plus a small margin, so a regression shows up here first.
-SQ8_RESTORE_BUDGET = {"sq8-avx512": 34, "sq8-avx2": 4}
+SQ8_RESTORE_BUDGET = {"sq8-avx512": 34, "sq8-avx2": 6}
 # scratch bytes the AVX-512-order SQ8 kernels may use (held to 128 VGPRs: a value or two live across
 # the query loop, stored at kernel entry and loaded after it -- never inside an expansion)
 SQ8_SCRATCH_BYTES = {"ip chunks=24": 12, "l2 chunks=24": 0, "ip chunks=30": 28, "l2 chunks=30": 12}
@@ -77,3 +77,30 @@ def test_register_budgets(census):
     assert census["ip chunks=24 stamp=0 space=sq8-avx512"]["NumVgprs"] <= 128
     for m in ("l2", "ip"):
         assert census[f"{m} chunks=4 stamp=0 space=f32"]["Occupancy"] >= 4
+
+
+@pytest.mark.parametrize("kernel", ["l2 chunks=4 stamp=4 space=f32", "ip chunks=4 stamp=4 space=f32",
+                                    "l2 chunks=8 stamp=4 space=f32",
+                                    "ip chunks=24 stamp=4 space=sq8-avx512", "l2 chunks=24 stamp=4 space=sq8-avx512"])
+def test_helper_kernels_keep_the_expansion_loop_clean(census, kernel):
+    """The distance-helper kernels (kMode 4: memo lookups in the expansion, the help loop after it) for
+    the SIFT shape (d = 128 / 256) and config 5 (768-d SQ8): no scratch traffic per expansion, few
+    SGPR restores, and the residency the searches were measured with."""
+    r = census[kernel]
+    assert r["expansion_loops"], "no expansion loop found"
+    # config 5's kernel (768-d IP) none; the 768-d L2 one (no benchmark shape) at most one
+    assert r["scratch_ops_in_expansion_loops"] <= (1 if kernel.startswith("l2 chunks=24") else 0), r
+    assert r["restores_in_expansion_loops"] <= 50, r  # measured 3 (f32), 40 / 48 (SQ8 IP / L2)
+    assert r["Occupancy"] >= (3 if "chunks=8" in kernel else 4), r
+
+
+@pytest.mark.parametrize("kernel", ["l2 chunks=30 stamp=8 space=f32", "ip chunks=30 stamp=8 space=f32",
+                                    "l2 chunks=24 stamp=8 space=f32"])
+def test_two_waves_wide_row_kernels(census, kernel):
+    """kMode 8: the wide-row f32 kernels at two waves per SIMD (one row per lane group) -- within
+    256 registers, no scratch, and the headline's one-wave kernel keeps its 24 rows per pass."""
+    r = census[kernel]
+    assert r["Occupancy"] >= 2 and r.get("ScratchSize", 0) == 0, r
+    assert r["restores_in_expansion_loops"] == 0, r
+    one = census[kernel.replace("stamp=8", "stamp=0")]
+    assert one["Occupancy"] == 1 and one.get("ScratchSize", 0) == 0, one

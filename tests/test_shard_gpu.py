@@ -27,12 +27,12 @@ def _free_port():
     return port
 
 
-def _run_ranks(tmp_path, world, n, dim, nq, k, ef, seed, mode="f32", backend="gloo"):
+def _run_ranks(tmp_path, world, n, dim, nq, k, ef, seed, mode="f32", backend="gloo", reserve_cus=0):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), ALAYA_TEST_BACKEND=backend)
+                   MASTER_PORT=str(port), ALAYA_TEST_BACKEND=backend, ALAYA_TEST_RESERVE_CUS=str(reserve_cus))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "shard_worker.py"), str(tmp_path),
                                        str(n), str(dim), str(nq), str(k), str(ef), str(seed), mode], env=env))
     try:
@@ -91,12 +91,15 @@ def test_sharded_sq8_ip_two_ranks(tmp_path):
     assert (ids[1] == lo1).sum() == 1
 
 
+@pytest.mark.parametrize("reserve", [0, 8])
 @pytest.mark.parametrize("mode", ["f32", "sq8"])
-def test_sharded_rccl_single_rank(tmp_path, mode):
+def test_sharded_rccl_single_rank(tmp_path, mode, reserve):
     """The RCCL backend itself (bench.py's N > 1 path on a node): init_process_group("nccl") with
     device_id, the device-tensor all_gather of packed keys, the merge sort and the double-buffered
     pipeline's exchange stream -- one rank, since a one-GPU box holds one RCCL rank.  With one shard
     the merged result is that shard's search (SQ8: plus the reference rerank, row 0 being global)."""
     dim, n = (768, 6000) if mode == "sq8" else (960, 6000)
-    parts = _run_ranks(tmp_path, 1, n, dim, 24, 10, 64, 33, mode, backend="nccl")
+    # reserve 8: the pipeline's search runs on a CU-masked stream (alaya_stream_create_reserving) and
+    # sizes its persistent grid to the CUs left, the exchange runs beside it -- same results
+    parts = _run_ranks(tmp_path, 1, n, dim, 24, 10, 64, 33, mode, backend="nccl", reserve_cus=reserve)
     _check(parts, 10)

@@ -120,9 +120,17 @@ def main():
                 ms = e0.elapsed_time(e1) / args.reps
                 h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
                 c = cnt.cpu().numpy()
+                hs = ""
+                if hasattr(dev, "help_stats"):
+                    st_ = dev.help_stats()
+                    m, x, hr = (tuple(st_) + (0, 0))[:3]
+                    if m:
+                        hs = (f"  memo {m / max(1, int(c[:, 0].sum())):.3f} of distances, "
+                              f"{x / max(1, int(c[:, 1].sum())):.3f} of expansions, "
+                              f"helper rows / memo hits {hr / max(1, m):.2f}")
                 print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb} spill-table {stb}"
                       f"{f' {env_name}={ev}' if env_name else ''}{f' [{var}]' if var != '-' else ''}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
-                      f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}", flush=True)
+                      f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}{hs}", flush=True)
     os.environ.pop("ALAYA_SEARCH_WAVES", None)
     os.environ.pop("ALAYA_MAX_WAVES_PER_CU", None)
     os.environ.pop("ALAYA_SPILL_TABLE", None)

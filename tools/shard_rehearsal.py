@@ -86,6 +86,13 @@ def main():
         shard_search(ix, lo, sq8, q, K, ef, ids, dd, cnt, stream.cuda_stream)
         e.record(stream)
         torch.cuda.synchronize()
+        if timed:  # the per-(shard, query group) breakdown: time, work and the launch's resident searchers
+            c = cnt.cpu().numpy().astype(np.int64)
+            g, w = ix.last_launch()
+            return a.elapsed_time(e), {"queries": m, "searchers": int(g) * int(w),
+                                       "rounds": round(m / max(1, int(g) * int(w)), 3),
+                                       "n_dist_sum": int(c[:, 0].sum()), "n_expand_mean": round(float(c[:, 1].mean()), 1),
+                                       "n_expand_max": int(c[:, 1].max())}
         return ids.cpu().numpy().astype(np.int64), dd.cpu().numpy().copy(), a.elapsed_time(e)
 
     results = []
@@ -109,15 +116,27 @@ def main():
         for lo, ix in shards:  # warm
             search(ix, lo, q_all[groups[0][0]:groups[0][1]], ef)
         worst = []
+        pairs = {}
         for _ in range(args.steps):
-            worst.append(max(search(ix, lo, q_all[qa:qb], ef)[2] for lo, ix in shards for qa, qb in groups))
+            step = []
+            for si, (lo, ix) in enumerate(shards):
+                for gi, (qa, qb) in enumerate(groups):
+                    t_ms, info = search(ix, lo, q_all[qa:qb], ef, timed=True)
+                    step.append(t_ms)
+                    pairs.setdefault((si, gi), {"shard": si, "group": gi, "ms": [], **info})["ms"].append(t_ms)
+            worst.append(max(step))
         ms = float(np.median(worst))
+        per_pair = []
+        for v in pairs.values():
+            v["kernel_ms"] = round(float(np.median(v.pop("ms"))), 3)
+            per_pair.append(v)
         row = {"shards": S, "query_groups": G, "ef": ef, "recall": next(x["recall"] for x in sweep if x["ef"] == ef),
                "queries_per_rank": groups[0][1] - groups[0][0], "max_rank_kernel_ms": round(ms, 3),
-               "predicted_qps": round(nq / (ms * 1e-3), 1), "sweep": sweep}
+               "predicted_qps": round(nq / (ms * 1e-3), 1), "per_rank": per_pair, "sweep": sweep}
         if S == 1:  # the one-GPU reference: the whole index, the whole batch
-            whole = [search(shards[0][1], 0, q_all, ef)[2] for _ in range(args.steps)]
-            row["one_gpu_qps"] = round(nq / (float(np.median(whole)) * 1e-3), 1)
+            whole = [search(shards[0][1], 0, q_all, ef, timed=True) for _ in range(args.steps)]
+            row["one_gpu_qps"] = round(nq / (float(np.median([w_[0] for w_ in whole])) * 1e-3), 1)
+            row["one_gpu"] = {"kernel_ms": round(float(np.median([w_[0] for w_ in whole])), 3), **whole[0][1]}
         results.append(row)
         print(json.dumps(row), flush=True)
         del shards
