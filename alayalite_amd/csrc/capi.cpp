@@ -180,7 +180,11 @@ void scratch_drain(alaya_index *ix) {
   hip_check(e, "hipEventSynchronize");
 }
 // guarded() for the entry points that launch searches on the index's scratch: a device error marks
-// the spill areas for re-zeroing.
+// the spill areas for re-zeroing.  This covers errors the call itself sees (launch failures, and the
+// synchronous entry points' syncs, scratch_drain).  A stream-async *_device call returns before its
+// kernel ends; a fault surfacing later (at a torch sync) is not seen here.  HIP errors from a device
+// fault are sticky -- the context is unusable and every later call of this index throws -- so no
+// later launch runs on tables a half-finished query left dirty.
 template <typename F>
 int guarded_scratch(alaya_index *ix, F &&f) {
   return guarded([&] {
@@ -359,9 +363,9 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0) +
                         (p.help ? alaya_amd::kHelpBoardBytes : 0);
   const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
-  // the register-bound residency, probed with a 4 KB table -- or with the smallest table when a
-  // spill table is the second level (a spill then costs a flush and prefetched bucket reads, not a
-  // round trip per visit, so residency wins over first-level size)
+  // the register-bound residency, probed with a 4 KB table.  The 1 KB probe applies only to the
+  // forced compact modes (1, 3) with a spill table: every other mode with a spill table returned
+  // set_mode(7) above.
   const bool stab = p.stab_log2 != 0;  // set by do_search (spill_table_log2)
   int vgpr_blocks = 0;
   hip_check(alaya_amd::search_occupancy(p, W, shared + W * (wave_fixed + (stab ? 1024 : 4096)), &vgpr_blocks),

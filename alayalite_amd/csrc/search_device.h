@@ -976,6 +976,12 @@ __device__ __forceinline__ void spill_prefetch(const Visited &vs, uint32_t row_v
 
 // End of a query: leave the slot's second level clean for the next one -- the spill table whole, and
 // the bitset's words on the dirty list (or the whole bitset when the list overflowed).  Wave-uniform.
+// The spill table is cleared whole on purpose: at its sizing (32 * ef entries, spill_table_log2) a
+// query's ~2.7k visited ids land in 1 - exp(-ids / buckets) of the buckets, ~73 % at config 5 (2^14
+// entries = 2,048 buckets, ef 368), so a dirty-bucket list would skip at most a quarter of a 32 KB
+// clear -- ~0.4 % of the launch's 21.6 GB -- and add a list store per first touch of a bucket plus
+// its SGPR state to an expansion loop that is at its register budget.  The clear is full 128-B lines
+// of coalesced stores (no read for ownership).
 __device__ __forceinline__ void visit_end(Visited &vs) {
   if (!vs.spilled) return;
   const int lane = lane_id();

@@ -42,11 +42,11 @@ def test_fixed_d_f32_expansion_loops_restore_no_spilled_sgpr(census, metric, chu
 
 
 # The AVX-512-order SQ8 kernels carry the spill table (round 4: flush, bucket prefetch, bitset third
-# level), whose uniform state costs SGPR restores per expansion -- 12-31 v_readlane against ~12k
-# cycles per expansion at config 5 (measured on this image's hipcc: 12 in config 5's 768-d IP
-# kernel, 31 in the others).  The AVX2-order kernels keep the bitset (0-6 restores).  Budgets are
-# the measured maxima plus a small margin, so a regression shows up here first.
-SQ8_RESTORE_BUDGET = {"sq8-avx512": 34, "sq8-avx2": 6}
+# level), whose uniform state costs SGPR restores per expansion -- 10-18 v_readlane against ~12k
+# cycles per expansion at config 5 (measured on this image's hipcc: 18 in config 5's 768-d IP
+# kernel, 10-17 in the others).  The AVX2-order kernels keep the bitset (2-6 restores).  Budgets
+# are the measured maxima plus a small margin, so a regression shows up here first.
+SQ8_RESTORE_BUDGET = {"sq8-avx512": 20, "sq8-avx2": 6}
 # scratch bytes the AVX-512-order SQ8 kernels may use (held to 128 VGPRs: a value or two live across
 # the query loop, stored at kernel entry and loaded after it -- never inside an expansion)
 SQ8_SCRATCH_BYTES = {"ip chunks=24": 12, "l2 chunks=24": 0, "ip chunks=30": 28, "l2 chunks=30": 12}
@@ -71,12 +71,17 @@ def test_register_budgets(census):
             assert r["scratch_ops_in_expansion_loops"] == 0, k
         if "sq8-avx512" in k and "chunks=0" not in k and "stamp=0" in k:
             budget = SQ8_SCRATCH_BYTES.get(k.split(" stamp")[0], 0)
-            assert r.get("ScratchSize", 0) <= budget and r["scratch_ops_total"] <= 8, (k, r.get("ScratchSize"))
+            # exactly the measured bytes: a new spilled value shows up here even outside the loops
+            assert r.get("ScratchSize", 0) == budget and r["scratch_ops_total"] <= 8, (k, r.get("ScratchSize"))
         elif "stamp=0" in k:
             assert r.get("ScratchSize", 0) == 0, k
     assert census["ip chunks=24 stamp=0 space=sq8-avx512"]["NumVgprs"] <= 128
     for m in ("l2", "ip"):
         assert census[f"{m} chunks=4 stamp=0 space=f32"]["Occupancy"] >= 4
+
+
+# SGPR restores per expansion in the helper kernels: measured 3 (f32), 40 / 48 (SQ8 IP / L2, 768-d)
+HELPER_RESTORE_BUDGET = {"chunks=4": 5, "chunks=8": 5, "chunks=24 sq8": 50}
 
 
 @pytest.mark.parametrize("kernel", ["l2 chunks=4 stamp=4 space=f32", "ip chunks=4 stamp=4 space=f32",
@@ -90,7 +95,8 @@ def test_helper_kernels_keep_the_expansion_loop_clean(census, kernel):
     assert r["expansion_loops"], "no expansion loop found"
     # config 5's kernel (768-d IP) none; the 768-d L2 one (no benchmark shape) at most one
     assert r["scratch_ops_in_expansion_loops"] <= (1 if kernel.startswith("l2 chunks=24") else 0), r
-    assert r["restores_in_expansion_loops"] <= 50, r  # measured 3 (f32), 40 / 48 (SQ8 IP / L2)
+    assert r["restores_in_expansion_loops"] <= HELPER_RESTORE_BUDGET[kernel.split(" stamp")[0].split(" ")[1] + (
+        " sq8" if "sq8" in kernel else "")], r
     assert r["Occupancy"] >= (3 if "chunks=8" in kernel else 4), r
 
 
