@@ -9,9 +9,12 @@ hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU-only buil
 
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import subprocess
 import sysconfig
+import time
 
 import pybind11
 
@@ -30,6 +33,29 @@ LIB_HEADERS = ["search_kernels.h", "search_device.h", "build_kernels.h", "flat_k
 EXT_SOURCES = ["pybind_module.cpp"]
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over the library's sources and headers, in a fixed order -- the
+    value compiled into libalaya_hip.so (alaya_build_info) and compared with the tree at run time, so
+    a stale or foreign library is visible in every bench line and smoke run."""
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, f) for f in LIB_SOURCES + LIB_HEADERS] + [os.path.join(INCLUDE, "alaya_hip.h")]:
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _hipcc_version() -> str:
+    try:
+        out = subprocess.run([HIPCC, "--version"], capture_output=True, text=True, check=True).stdout
+    except (OSError, subprocess.CalledProcessError):
+        return "unknown"
+    for line in out.splitlines():
+        if "HIP version" in line or "clang version" in line:
+            return line.strip()
+    return out.splitlines()[0].strip() if out else "unknown"
+
+
 def _newer(target: str, deps: list[str]) -> bool:
     if not os.path.exists(target):
         return True
@@ -46,11 +72,16 @@ def _run(cmd: list[str], verbose: bool) -> None:
 def build(force: bool = False, verbose: bool = False) -> tuple[str, str]:
     lib_deps = [os.path.join(CSRC, f) for f in LIB_SOURCES + LIB_HEADERS] + [os.path.join(INCLUDE, "alaya_hip.h")]
     if force or _newer(LIB, lib_deps):
+        src_hash = source_hash()
+        hipcc = "".join(c if c.isalnum() or c in ".-+:()" else "_" for c in _hipcc_version())
+        info = f"source={src_hash} arch={ARCH} hipcc={hipcc} built={time.strftime('%Y-%m-%dT%H:%M:%SZ', time.gmtime())}"
         objs, procs = [], []
         for src in LIB_SOURCES:  # compile translation units concurrently
             obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
             flags = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-pthread",
                      f"-I{INCLUDE}", "-c", os.path.join(CSRC, src), "-o", obj]
+            if src == "capi.cpp":  # alaya_build_info()
+                flags.insert(1, f'-DALAYA_BUILD_INFO="{info}"')
             if src.endswith(".hip"):
                 flags[1:1] = ["-x", "hip", f"--offload-arch={ARCH}"]
                 # diagnostic builds only (e.g. -DALAYA_FINE_STAMPS for tools/profile_phases.py)
@@ -65,6 +96,8 @@ def build(force: bool = False, verbose: bool = False) -> tuple[str, str]:
         _run([HIPCC, "-shared", "-fPIC", "-pthread", "-o", LIB] + objs + ["-lamdhip64"], verbose)
         for o in objs:
             os.remove(o)
+        with open(os.path.join(HERE, "BUILD_INFO.json"), "w") as fh:
+            json.dump({"source_hash": src_hash, "arch": ARCH, "hipcc": hipcc, "info": info}, fh)
     ext_deps = [os.path.join(CSRC, f) for f in EXT_SOURCES + ["host_distance.h"]] + [LIB]
     if force or _newer(EXT, ext_deps):
         py_inc = sysconfig.get_paths()["include"]

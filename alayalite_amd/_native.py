@@ -46,3 +46,18 @@ IndexType = _ext.IndexType
 MetricType = _ext.MetricType
 QuantizationType = _ext.QuantizationType
 device_count = _ext.device_count
+
+
+def build_provenance() -> dict:
+    """Which sources the loaded library was compiled from (alaya_build_info) against the sources in
+    this tree now: a stale library -- sources edited after the build, or a library from another
+    tree -- shows as library_matches_tree = False in every bench line and smoke run."""
+    from alayalite_amd import _build
+
+    info = _ext.build_info()
+    fields = dict(kv.split("=", 1) for kv in info.split() if "=" in kv)
+    lib_hash = fields.get("source", "unknown")
+    tree_hash = _build.source_hash()
+    return {"library": info, "library_source_hash": lib_hash, "tree_source_hash": tree_hash,
+            "library_matches_tree": lib_hash == tree_hash,
+            "library_path": os.path.join(_HERE, "libalaya_hip.so")}

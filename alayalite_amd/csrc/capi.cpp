@@ -658,6 +658,11 @@ extern "C" {
 
 const char *alaya_last_error(void) { return g_last_error.c_str(); }
 
+#ifndef ALAYA_BUILD_INFO
+#define ALAYA_BUILD_INFO "source=unknown"
+#endif
+const char *alaya_build_info(void) { return ALAYA_BUILD_INFO; }
+
 int alaya_device_count(int *count) {
   return guarded([&] {
     int c = 0;

@@ -1018,6 +1018,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
     return codes;
   }, py::arg("data"), py::arg("min"), py::arg("max"), py::arg("num_threads") = 1u);
   m.def("host_sq8_order", &host_sq8_order);
+  m.def("build_info", [] { return std::string(alaya_build_info()); });
   m.def("device_count", [] {
     int c = 0;
     check(alaya_device_count(&c));

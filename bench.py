@@ -477,6 +477,7 @@ def run_flat(args):
                                      "bf16 MFMA dense peak 16 x 157.3 TF / 3 bf16 products per f32 product "
                                      "(MI355X_MICROARCH.md)")},
         "cpu_baseline": cpu,
+        "build": _native.build_provenance(),
     }
     print(json.dumps(out), flush=True)
 
@@ -841,6 +842,8 @@ def main():
                          "mean_n_dist": round(float(cnt[:, 0].mean()), 1),
                          "mean_n_expand": round(float(cnt[:, 1].mean()), 1)},
             "cpu_baseline": cpu,
+            # which sources the loaded libalaya_hip.so was compiled from, against this tree's
+            "build": _native.build_provenance(),
         }
         if curve is not None:
             out["config"]["qps_curve"] = curve

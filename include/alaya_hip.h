@@ -60,6 +60,10 @@ typedef struct alaya_index alaya_index;
 typedef struct alaya_graph alaya_graph;
 
 const char *alaya_last_error(void);
+/* Build provenance (no reference counterpart): "source=<16 hex digits of sha256 over the library's
+ * sources and headers> arch=gfx950 hipcc=<compiler> built=<UTC time>", fixed when the library was
+ * compiled (alayalite_amd/_build.py).  bench.py and smoke() compare the source hash with the tree. */
+const char *alaya_build_info(void);
 /* Number of visible HIP devices (0 when none). */
 int alaya_device_count(int *count);
 /* Roofline calibration (no reference counterpart): the best of `iters` streaming reads of a

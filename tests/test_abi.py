@@ -55,3 +55,17 @@ def test_import_starts_no_gpu_runtime():
     env.pop("ALAYA_SKIP_TORCH_INIT", None)
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_build_provenance_matches_tree(native):
+    """The library carries the hash of the sources it was compiled from (alaya_build_info), and the
+    in-tree library is current: built from the sources in this tree."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "alayalite_amd", "libalaya_hip.so"))
+    lib.alaya_build_info.restype = ctypes.c_char_p
+    info = lib.alaya_build_info().decode()
+    assert info.startswith("source=") and "arch=gfx950" in info, info
+    from alayalite_amd import _native
+
+    prov = _native.build_provenance()
+    assert prov["library"] == info
+    assert prov["library_matches_tree"], prov
