@@ -73,7 +73,7 @@ def test_config4_gist_1m(native, orc, gist1m, nq):
     ids, dists, cnt = dev.search(qs, K, 373)
     grid, waves = dev.last_launch()
     if nq == 1_250:  # past 1,024 resident one-wave searchers, below 1.5x: the two-waves kernel
-        assert grid * waves > 1_250, (grid, waves)
+        assert grid * waves >= 1_250, (grid, waves)  # (the grid is capped at the batch)
     view = _view(orc, g, base)
     _check(view, qs, ids, dists, cnt, 373, _sample(nq, spread=120, tail=30))
 
