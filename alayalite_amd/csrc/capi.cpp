@@ -502,13 +502,14 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     p.wave_lds = static_cast<uint32_t>(alaya_amd::search_wave_lds_bytes(ix->stride, ef, p.hash_log2, compact));
     bool fits = true;
     if (p.help) {
-      // the memo (W searchers x 3 requests x R entries of 8 bytes) overlays the memo wave's query
-      // vector, or else its pool and visited table
+      // the memo (W searchers x kHelpMemoSlots requests x R entries of 8 bytes) overlays the memo
+      // wave's query vector, or else its pool and visited table (past the query and the three
+      // 64-entry lists the helper still uses)
       const size_t need = static_cast<size_t>(W) * alaya_amd::kHelpMemoSlots * ix->R * 8;
       const size_t q_bytes = static_cast<size_t>(ix->stride) * 4;
       if (q_bytes >= need) {
         p.memo_off = 0;
-      } else if (p.wave_lds - (q_bytes + 3 * 64 * 4) >= need) {
+      } else if (p.wave_lds >= q_bytes + 3 * 64 * 4 + need) {
         p.memo_off = static_cast<uint32_t>(q_bytes + 3 * 64 * 4);
       } else {
         fits = false;

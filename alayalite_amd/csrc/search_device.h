@@ -679,12 +679,18 @@ __device__ __forceinline__ void compact_key(const Visited &vs, uint32_t v, uint3
   }
 }
 
+// kShared: the table belongs to another wave that may be writing it (the distance helpers' visited
+// hint, search_kernels.hip): its slots are read as relaxed workgroup-scope atomics, and the answer is
+// a hint that may be stale either way.  The probe still ends: a table holds at most vis_limit + 64 <
+// slots entries (a wide probe meets an empty slot) and a compact probe stops at max_disp.
+template <bool kShared = false>
 __device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
   const uint32_t mask = (1u << vs.log2h) - 1u;
   if (vs.rbits == kVisWide) {
     uint32_t h = hash_slot(v, vs.log2h);
     for (;;) {
-      const uint32_t e = vs.tab[h];
+      const uint32_t e = kShared ? __hip_atomic_load(&vs.tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                 : vs.tab[h];
       if (e == v) return true;
       if (e == kEmpty) return false;
       h = (h + 1) & mask;
@@ -694,7 +700,9 @@ __device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
   compact_key(vs, v, home, rem);
   const uint16_t *t16 = reinterpret_cast<const uint16_t *>(vs.tab);
   for (uint32_t i = 0;; ++i) {
-    const uint32_t e = t16[(home + i) & mask];
+    const uint32_t e = kShared ? __hip_atomic_load(&t16[(home + i) & mask], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP)
+                               : t16[(home + i) & mask];
     if (e == 0u) return false;
     if (e == 1u + ((i << vs.rbits) | rem)) return true;
     if (i == vs.max_disp) return false;  // inserts never go further

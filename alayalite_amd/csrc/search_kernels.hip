@@ -436,7 +436,7 @@ __device__ __forceinline__ uint64_t *help_memo(const SearchParams &p, unsigned c
 template <int kSpace>
 __device__ __forceinline__ bool sibling_visited(const SearchParams &p, const Lds &Lt, int t, uint32_t v, bool want) {
   Visited vt = make_visited(p, Lt.hash, nullptr, nullptr, nullptr);
-  bool seen = want && table_lookup(vt, v);
+  bool seen = want && table_lookup<true>(vt, v);
   if constexpr (space_tab<kSpace>()) {
     if (p.spill_table != nullptr) {
       const uint64_t slot = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + t;
