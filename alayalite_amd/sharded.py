@@ -281,6 +281,13 @@ class ShardPipeline:
             _ext.stream_destroy(self._masked)
             self._masked = None
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     def search_ms(self):
         """Mean search time (ms) of the batches run with timing=True, as the compute stream saw it
         inside the pipeline (after synchronisation)."""

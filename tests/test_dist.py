@@ -151,9 +151,9 @@ def _pipeline_worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rng = np.random.default_rng(7)
     batches = [torch.from_numpy(rng.random((23, 8), dtype=np.float32)) for _ in range(5)]
-    pipe = ShardPipeline(_fake_search(rank, 10), 23, 10, rank * 300, "cpu")
-    over = pipe.run(batches)
-    sync = pipe.run_sync(batches)
+    with ShardPipeline(_fake_search(rank, 10), 23, 10, rank * 300, "cpu") as pipe:  # (close() on exit)
+        over = pipe.run(batches)
+        sync = pipe.run_sync(batches)
     if rank == 0:
         np.savez(out_path, over_i=np.stack([o[0].numpy() for o in over]), over_d=np.stack([o[1].numpy() for o in over]),
                  sync_i=np.stack([o[0].numpy() for o in sync]), sync_d=np.stack([o[1].numpy() for o in sync]),
