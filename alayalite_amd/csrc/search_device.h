@@ -357,6 +357,11 @@ __device__ __forceinline__ void sq8_chunk(const float *xq, const float *sc, cons
   acc[3] = sq8_term<kIP>(x.w, s.w, mn.w, static_cast<float>(w >> 24), acc[3]);
 }
 
+#ifndef ALAYA_PAIR_LOOPS
+// lane loops over ballot masks take two lanes per trip (pool_merge's LDS path, stab_visit): config 5
+// 1k queries 3.60 -> 3.53 ms, 10k 9.51 -> 9.47 ms, GIST unchanged (profiles/r05/pair/)
+#define ALAYA_PAIR_LOOPS 1
+#endif
 #ifndef ALAYA_SQ8_DW
 #define ALAYA_SQ8_DW 48  // code dwords in flight per lane (rows per lane group = DW / chunks)
 #endif
@@ -838,10 +843,23 @@ __device__ __forceinline__ bool stab_visit(Visited &vs, uint32_t v, bool act, bo
   const bool fast = act && !found && occ < kStabBucket;
   const uint64_t fm = ballot(fast);
   uint32_t rank = 0;
+#if ALAYA_PAIR_LOOPS
+  for (uint64_t r = fm; r;) {  // two fast lanes per trip (see pool_merge)
+    const int j = __ffsll(static_cast<unsigned long long>(r)) - 1;
+    r &= r - 1;
+    const bool t2 = r != 0ull;
+    const int j2 = t2 ? __ffsll(static_cast<unsigned long long>(r)) - 1 : j;
+    r &= t2 ? r - 1 : r;
+    const uint32_t h1 = read_lane(home, j), h2 = read_lane(home, j2);
+    rank += (j < lane && h1 == home) ? 1u : 0u;
+    rank += (t2 && j2 < lane && h2 == home) ? 1u : 0u;
+  }
+#else
   for (uint64_t r = fm; r; r &= r - 1) {
     const int j = __ffsll(static_cast<unsigned long long>(r)) - 1;
     rank += (j < lane && read_lane(home, j) == home) ? 1u : 0u;
   }
+#endif
   const bool placed = fast && occ + rank < kStabBucket;
   if (placed) stab_store(vs, home * kStabBucket + occ + rank, code);
   // rare: the home bucket is full (v may be in the bitset) or filled up within this visit (v is
@@ -1081,6 +1099,8 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
     if (!ballot((acc && d != d) || (v0 && p0 != p0) || (v1 && p1 != p1))) {
       uint32_t rank = 0, pos = 0, s0 = 0, s1 = 0;
       uint64_t rest = amask;
+      // (one lane per trip: the paired loop of the LDS path below was 4-5 % slower here, SIFT-shaped
+      // 1M at 10k / 1k queries, profiles/r05/pair/)
       while (rest) {
         const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
         rest &= rest - 1;
@@ -1119,12 +1139,26 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   // stable rank of this candidate among accepted ones, ordered by (dist, arrival)
   uint32_t rank = 0;
   uint64_t rest = amask;
+#if ALAYA_PAIR_LOOPS
+  while (rest) {  // two accepted lanes per trip (see the register merge above)
+    const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
+    rest &= rest - 1;
+    const bool t2 = rest != 0ull;
+    const int j2 = t2 ? __ffsll(static_cast<unsigned long long>(rest)) - 1 : j;
+    rest &= t2 ? rest - 1 : rest;
+    const float dj = read_lane(d, j);
+    const float dj2 = read_lane(d, j2);
+    rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
+    rank += (t2 && (dj2 < d || (dj2 == d && j2 < lane))) ? 1u : 0u;
+  }
+#else
   while (rest) {
     const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
     rest &= rest - 1;
     const float dj = read_lane(d, j);
     rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
   }
+#endif
   if (acc) L.sd[rank] = d;
   uint32_t pos = 0;
   if (acc) pos = pool_upper_bound(L.pd, ps.size, d) + rank;

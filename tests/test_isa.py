@@ -42,11 +42,12 @@ def test_fixed_d_f32_expansion_loops_restore_no_spilled_sgpr(census, metric, chu
 
 
 # The AVX-512-order SQ8 kernels carry the spill table (round 4: flush, bucket prefetch, bitset third
-# level), whose uniform state costs SGPR restores per expansion -- 10-18 v_readlane against ~12k
-# cycles per expansion at config 5 (measured on this image's hipcc: 18 in config 5's 768-d IP
-# kernel, 10-17 in the others).  The AVX2-order kernels keep the bitset (2-6 restores).  Budgets
-# are the measured maxima plus a small margin, so a regression shows up here first.
-SQ8_RESTORE_BUDGET = {"sq8-avx512": 20, "sq8-avx2": 6}
+# level), whose uniform state costs SGPR restores per expansion -- 10-21 v_readlane against ~12k
+# cycles per expansion at config 5 (measured on this image's hipcc: 21 in config 5's 768-d IP
+# kernel since the paired lane loops, 10-17 in the others).  The AVX2-order kernels keep the bitset
+# (2-6 restores).  Budgets are the measured maxima plus a small margin, so a regression shows up
+# here first.
+SQ8_RESTORE_BUDGET = {"sq8-avx512": 23, "sq8-avx2": 6}
 # scratch bytes the AVX-512-order SQ8 kernels may use (held to 128 VGPRs: a value or two live across
 # the query loop, stored at kernel entry and loaded after it -- never inside an expansion)
 SQ8_SCRATCH_BYTES = {"ip chunks=24": 12, "l2 chunks=24": 0, "ip chunks=30": 28, "l2 chunks=30": 12}
