@@ -7,6 +7,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# A/B runs (tools/build_ab.sh): the parity tests against a saved variant build of the package
+AB_ROOT = os.environ.get("ALAYA_AB_ROOT")
+if AB_ROOT:
+    sys.path.insert(0, AB_ROOT)
 
 
 def pytest_configure(config):
@@ -23,9 +27,10 @@ def native():
         torch.cuda.is_available()
     except Exception:  # pragma: no cover - torch is optional for the engine itself
         pass
-    from alayalite_amd import _build
+    if not AB_ROOT:  # (a saved variant is prebuilt and has no sources)
+        from alayalite_amd import _build
 
-    _build.build()
+        _build.build()
     from alayalite_amd import _native
 
     return _native._ext
