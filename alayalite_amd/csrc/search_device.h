@@ -357,11 +357,6 @@ __device__ __forceinline__ void sq8_chunk(const float *xq, const float *sc, cons
   acc[3] = sq8_term<kIP>(x.w, s.w, mn.w, static_cast<float>(w >> 24), acc[3]);
 }
 
-#ifndef ALAYA_SQ8_REG_MERGE
-// pool entries per lane of a register merge in the plain (no helpers) AVX-512-order SQ8 kernels;
-// 0 = the LDS merge (diagnostics builds only: with the helpers' registers it spilled)
-#define ALAYA_SQ8_REG_MERGE 0
-#endif
 #ifndef ALAYA_PAIR_LOOPS
 // lane loops over ballot masks take two lanes per trip (pool_merge's LDS path, stab_visit): config 5
 // 1k queries 3.60 -> 3.53 ms, 10k 9.51 -> 9.47 ms, GIST unchanged (profiles/r05/pair/)
@@ -1077,7 +1072,7 @@ struct NoMark {
   __device__ void operator()() const {}
 };
 
-template <int kRegSlots = 0, typename OnNext = NoNext, typename Mark = NoMark>
+template <bool kRegMerge = false, typename OnNext = NoNext, typename Mark = NoMark>
 __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, float d,
                            OnNext on_next = OnNext(), Mark mark = Mark()) {
   const int lane = lane_id();
@@ -1087,7 +1082,7 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
   const uint64_t amask = ballot(acc);
   const uint32_t n_acc = __popcll(amask);
   if (n_acc == 0) return;
-  if (kRegSlots == 2 && ps.ef <= 128) {
+  if (kRegMerge && ps.ef <= 128) {
     // Pools of up to 128 entries (ef <= 128: SIFT-shaped searches) merge from registers: lane l
     // holds entries l and 64 + l, and one pass over the accepted lanes yields every candidate's
     // rank, its upper bound in the pool (a ballot count, == the binary search on a sorted pool)
@@ -1130,69 +1125,6 @@ __device__ void pool_merge(PoolState &ps, const Lds &L, bool has, uint32_t id, f
       if (v1 && s1 != 0 && lane + 64 + s1 < ps.ef) {
         L.pd[lane + 64 + s1] = p1;
         L.pi[lane + 64 + s1] = i1;
-      }
-      if (acc && pos < ps.ef) {
-        L.pd[pos] = d;
-        L.pi[pos] = id;
-      }
-      wave_sync();
-      ps.size = min(size + n_acc, ps.ef);
-      if (first_pos < ps.cur) ps.cur = first_pos;
-      return;
-    }
-  }
-  if (kRegSlots > 2 && ps.ef <= 64u * kRegSlots) {
-    // Larger pools (diagnostics builds, ALAYA_SQ8_REG_MERGE): kRegSlots entries per lane, the same
-    // one-pass scheme.  An entry past the pool's size holds a NaN (it compares false both ways: no
-    // upper bound, no shift), the shifts are packed four to a register and the ids are read after
-    // the candidate loop, to keep the registers live across it few.
-    constexpr int S = kRegSlots > 2 ? kRegSlots : 1;
-    const uint32_t size = ps.size;
-    float pk[S];
-    bool nan = acc && d != d;
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-      const bool vk = static_cast<uint32_t>(lane) + 64u * k < size;
-      const float x = vk ? L.pd[lane + 64 * k] : 0.f;
-      nan = nan || x != x;
-      pk[k] = vk ? x : __builtin_nanf("");
-    }
-    if (!ballot(nan)) {
-      constexpr int SP = (S + 3) / 4;
-      uint32_t rank = 0, pos = 0, shp[SP];
-#pragma unroll
-      for (int k = 0; k < SP; ++k) shp[k] = 0u;
-      uint64_t rest = amask;
-      while (rest) {
-        const int j = __ffsll(static_cast<unsigned long long>(rest)) - 1;
-        rest &= rest - 1;
-        const float dj = read_lane(d, j);
-        rank += (dj < d || (dj == d && j < lane)) ? 1u : 0u;
-        uint32_t ub = 0;
-#pragma unroll
-        for (int k = 0; k < S; ++k) {
-          ub += __popcll(ballot(pk[k] <= dj));
-          shp[k / 4] += dj < pk[k] ? (1u << (8 * (k % 4))) : 0u;
-        }
-        if (lane == j) pos = ub;
-      }
-      pos += rank;
-      const int lane0 = __ffsll(static_cast<unsigned long long>(ballot(acc && rank == 0))) - 1;
-      const uint32_t first_pos = read_lane(pos, lane0);
-      if (first_pos <= ps.cur) on_next(read_lane(id, lane0));
-      mark();
-      uint32_t ik[S];
-#pragma unroll
-      for (int k = 0; k < S; ++k) ik[k] = ((shp[k / 4] >> (8 * (k % 4))) & 0xffu) != 0 ? L.pi[lane + 64 * k] : 0u;
-      wave_sync();
-#pragma unroll
-      for (int k = 0; k < S; ++k) {
-        const uint32_t shk = (shp[k / 4] >> (8 * (k % 4))) & 0xffu;
-        const uint32_t dst = static_cast<uint32_t>(lane) + 64u * k + shk;
-        if (shk != 0 && dst < ps.ef) {
-          L.pd[dst] = pk[k];
-          L.pi[dst] = ik[k];
-        }
       }
       if (acc && pos < ps.ef) {
         L.pd[pos] = d;

@@ -643,8 +643,7 @@ __global__ void __launch_bounds__(256)
     // Register merge (pool_merge, pools of <= 128 entries) in the small-row f32 kernels, whose ef
     // at recall 0.95 is ~70 (SIFT-shaped); the SQ8 / wide-row kernels run ef ~370 and keep their
     // registers for the row pass.
-    constexpr int kRegMerge = (kSpace == 0 && kChunks > 0 && kChunks <= 8) ? 2
-                              : (kSpace == 2 && kChunks > 0 && !(kMode & 4)) ? ALAYA_SQ8_REG_MERGE : 0;
+    constexpr bool kRegMerge = kSpace == 0 && kChunks > 0 && kChunks <= 8;
     uint32_t pre_u = kEmpty;
     uint64_t pre_lo = 0ull, pre_hi = 0ull;
     while (ps.cur < ps.size) {
