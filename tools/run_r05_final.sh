@@ -5,7 +5,7 @@
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 source tools/gpu_steps.sh
-step 700 gpurun_out/r05f_suite.log python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread
+step 900 gpurun_out/r05f_suite.log python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread
 step 300 gpurun_out/r05f_smoke.log python -u -c "import __graft_entry__ as g; g.smoke()"
 bash tools/run_bench_1m.sh || exit $?
 cat gpurun_out/bench_1m.json
