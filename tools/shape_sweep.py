@@ -36,6 +36,10 @@ def main():
     ap.add_argument("--envs", default="", help="environment variants: comma-separated, each '-' (none) or "
                                                "NAME=VAL+NAME=VAL...; applied on top of --env-sweep")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--order", default="batch",
+                    help="query orders (comma-separated): batch; xcd = queries grouped by their nearest of 256 "
+                         "pivot rows, group chunk x at positions = x mod 8 (the first round's XCD); sorted = "
+                         "grouped contiguously.  ids are compared in batch order")
     args = ap.parse_args()
     import torch
 
@@ -59,10 +63,29 @@ def main():
     if sq8:
         mn, mx = ext.sq8_train(base)
         dev.set_sq8(ext.sq8_encode(base, mn, mx, 16), mn, mx, ext.host_sq8_order())
+    piv = base[np.random.default_rng(11).choice(base.shape[0], 256, replace=False)].astype(np.float32)
     del base
+
+    def order_perm(kind, nq):
+        if kind == "batch":
+            return np.arange(nq)
+        q = queries[:nq].astype(np.float32)
+        sc = q @ piv.T if metric == 1 else 2 * (q @ piv.T) - (piv * piv).sum(1)[None, :]
+        key = np.argmax(sc, axis=1)
+        srt = np.argsort(key, kind="stable")
+        if kind == "sorted":
+            return srt
+        chunks = np.array_split(srt, 8)  # chunk x -> positions x, x + 8, ...
+        perm = np.empty(nq, np.int64)
+        for x, c in enumerate(chunks):
+            pos = np.arange(x, nq, 8)[: len(c)]
+            perm[pos] = c[: len(pos)]
+        return perm
+
     st = torch.cuda.current_stream()
-    for nq in [int(x) for x in args.nq.split(",")]:
-        qd = torch.from_numpy(np.ascontiguousarray(queries[:nq])).cuda()
+    for nq, order in [(int(x), o) for x in args.nq.split(",") for o in args.order.split(",")]:
+        perm = order_perm(order, nq)
+        qd = torch.from_numpy(np.ascontiguousarray(queries[:nq][perm])).cuda()
         ids = torch.empty((nq, 10), dtype=torch.int32, device="cuda")
         dd = torch.empty((nq, 10), dtype=torch.float32, device="cuda")
         cnt = torch.empty((nq, 4), dtype=torch.int32, device="cuda")
@@ -118,7 +141,9 @@ def main():
                 e1.record(st)
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / args.reps
-                h = int(np.bitwise_xor.reduce(ids.cpu().numpy().astype(np.int64).ravel() * 2654435761 % (1 << 31)))
+                ids_b = np.empty((nq, 10), np.int64)
+                ids_b[perm] = ids.cpu().numpy()
+                h = int(np.bitwise_xor.reduce(ids_b.ravel() * 2654435761 % (1 << 31)))
                 c = cnt.cpu().numpy()
                 hs = ""
                 if hasattr(dev, "help_stats"):
@@ -128,7 +153,7 @@ def main():
                         hs = (f"  memo {m / max(1, int(c[:, 0].sum())):.3f} of distances, "
                               f"{x / max(1, int(c[:, 1].sum())):.3f} of expansions, "
                               f"helper rows / memo hits {hr / max(1, m):.2f}")
-                print(f"nq {nq} waves {w} max/CU {mw} visited {vm} table {tb} spill-table {stb}"
+                print(f"nq {nq}{'' if order == 'batch' else ' order ' + order} waves {w} max/CU {mw} visited {vm} table {tb} spill-table {stb}"
                       f"{f' {env_name}={ev}' if env_name else ''}{f' [{var}]' if var != '-' else ''}: {ms:.3f} ms  {nq / ms * 1e3:,.0f} QPS  ids-hash {h}  "
                       f"n_dist {c[:, 0].mean():.1f} n_expand {c[:, 1].mean():.1f}{hs}", flush=True)
     os.environ.pop("ALAYA_SEARCH_WAVES", None)
