@@ -73,7 +73,8 @@ struct SearchParams {
   const float *sq_max;
   // distance helpers (search_has_helpers): 1 = a wave with no query left computes its workgroup
   // siblings' next distances into an LDS memo (kHelpBoardBytes after the wave regions); help_flags
-  // are diagnostics (ALAYA_HELP_FLAGS bit 0 = helpers compute every claimed row, no visited hint)
+  // are diagnostics (ALAYA_HELP_FLAGS bit 0 = no visited hint: helpers compute every claimed row;
+  // bit 1 = the hint in the f32 kernels too -- by default only the SQ8 kernels use it)
   uint32_t help;
   uint32_t help_flags;
   uint32_t memo_off;      // byte offset of a helper's memo in its wave region (0: the query vector)
