@@ -686,18 +686,22 @@ __device__ __forceinline__ void compact_key(const Visited &vs, uint32_t v, uint3
 
 // kShared: the table belongs to another wave that may be writing it (the distance helpers' visited
 // hint, search_kernels.hip): its slots are read as relaxed workgroup-scope atomics, and the answer is
-// a hint that may be stale either way.  The probe still ends: a table holds at most vis_limit + 64 <
-// slots entries (a wide probe meets an empty slot) and a compact probe stops at max_disp.
+// a hint that may be stale either way.  The owner's own probe ends because a table holds at most
+// vis_limit + 64 < slots entries (a wide probe meets an empty slot) and a compact probe stops at
+// max_disp.  A shared wide probe is also bounded by the table size: the region may be overwritten
+// under it (a sibling that just ran out of queries clears its memo area over its table, and a zeroed
+// wide table has no kEmpty slot), so it gives up after one lap.
 template <bool kShared = false>
 __device__ __forceinline__ bool table_lookup(const Visited &vs, uint32_t v) {
   const uint32_t mask = (1u << vs.log2h) - 1u;
   if (vs.rbits == kVisWide) {
     uint32_t h = hash_slot(v, vs.log2h);
-    for (;;) {
+    for (uint32_t i = 0;; ++i) {
       const uint32_t e = kShared ? __hip_atomic_load(&vs.tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
                                  : vs.tab[h];
       if (e == v) return true;
       if (e == kEmpty) return false;
+      if (kShared && i == mask) return false;
       h = (h + 1) & mask;
     }
   }

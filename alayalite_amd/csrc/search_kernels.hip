@@ -284,9 +284,9 @@ __device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, c
 // interleave (include/executor/worker.hpp:47,111-136); here the batch tail's idle waves (and, in
 // batches smaller than the resident searchers, the spare ones) shorten the remaining searchers'
 // expansions instead.
-// LDS: a 208-byte board after the workgroup's wave regions; the memo (W x 3 x R entries of 8 bytes)
-// at byte p.memo_off of the memo wave's region -- its query vector or its pool and visited table,
-// unused once it has no query.
+// LDS: a kHelpBoardBytes (256-byte) board after the workgroup's wave regions; the memo (W x kHelpSlots
+// x R entries of 8 bytes) at byte p.memo_off of the memo wave's region -- its query vector or its pool
+// and visited table, unused once it has no query.
 // --------------------------------------------------------------------------------------------
 // How far ahead a searcher asks: 1 = the next expansion, 2 = the next two (diagnostics builds:
 // -DALAYA_HELP_DEPTH=2).  One slot more than the depth keeps the expanding node's request alive
@@ -424,7 +424,8 @@ __device__ __forceinline__ void mine_reset(HelpBoard *b, int wave, HelpMine &m) 
   help_reset(b, wave);
 }
 
-// The memo: W x 2 x R entries (seq << 32 | distance bits) at p.memo_off of the memo wave's region.
+// The memo: W x kHelpSlots x R entries (seq << 32 | distance bits) at p.memo_off of the memo wave's
+// region.
 template <int kSpace>
 __device__ __forceinline__ uint64_t *help_memo(const SearchParams &p, unsigned char *smem, int memo_wave) {
   return reinterpret_cast<uint64_t *>(reinterpret_cast<unsigned char *>(carve_lds<kSpace>(p, smem, memo_wave).q) +
@@ -470,7 +471,18 @@ __device__ void help_siblings(const SearchParams &p, unsigned char *smem, const 
   const bool hint = (p.help_flags & 2u) || (space_sq8<kSpace>() && !(p.help_flags & 1u));
   uint32_t *exhausted = reinterpret_cast<uint32_t *>(L.sd);  // per (sibling, slot): a request fully claimed
   if (lane < 4 * kHelpSlots) exhausted[lane] = 0u;
-  // the first helper's region holds the memo: clear this wave's (seq 0 = no entry), then claim the role
+  // Leave the searchers first: retire this wave's last requests and set its helper bit, so no helper
+  // that reads the board from now on picks this wave as a sibling.  Only then may its region be
+  // overwritten by the memo clear below (with memo_off > 0 it covers the pool and the visited
+  // table, which another helper's visited hint reads; a helper that read the board just before
+  // still probes a bounded lap, table_lookup<true>).
+  help_reset(b, wave);
+  wave_sync();
+  if (lane == 0) __hip_atomic_fetch_or(&b->mask, 1u << wave, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  wave_sync();
+  // the first helper's region holds the memo: clear this wave's (seq 0 = no entry), then claim the
+  // role (no helper reads the memo before some wave has claimed it: each claims or finds it claimed
+  // before its own loop, and a searcher looks only once the role is set)
   {
     uint64_t *mine = help_memo<kSpace>(p, smem, wave);
     for (uint32_t e = lane; e < static_cast<uint32_t>(W) * kHelpSlots * R; e += 64)
@@ -481,11 +493,10 @@ __device__ void help_siblings(const SearchParams &p, unsigned char *smem, const 
     uint32_t cur = __hip_atomic_load(&b->mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     while ((cur >> 8) == 0u) {
       const uint32_t want = cur | (static_cast<uint32_t>(wave + 1) << 8);
-      const uint32_t old = atomicCAS(&b->mask, cur, want);
-      if (old == cur) break;
-      cur = old;
+      if (__hip_atomic_compare_exchange_strong(&b->mask, &cur, want, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP))
+        break;
     }
-    __hip_atomic_fetch_or(&b->mask, 1u << wave, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   wave_sync();
   int t = wave;

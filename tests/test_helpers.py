@@ -39,12 +39,13 @@ def sift_like(native, orc):
     return base, queries, g, view
 
 
-@pytest.mark.parametrize("hint", ["0", "1"])
+@pytest.mark.parametrize("hint", ["1", "2"])
 @pytest.mark.parametrize("ef", [40, 128])
 def test_helped_small_batches_bit_exact(native, sift_like, monkeypatch, ef, hint):
     """d = 128 L2 (the SIFT kernel), batches of 1 .. 600 queries: most workgroups run one searcher
-    and three helpers.  hint "1" (ALAYA_HELP_FLAGS=1): helpers compute every claimed row, without
-    looking the sibling's visited set up first."""
+    and three helpers.  ALAYA_HELP_FLAGS (search_kernels.hip, help_siblings): bit 0 forces the
+    visited hint off, bit 1 forces it on.  "1": helpers compute every claimed row (the f32 default);
+    "2": they first look each id up in the sibling's LDS table (table_lookup<true>)."""
     base, queries, g, view = sift_like
     monkeypatch.setenv("ALAYA_HELP_FLAGS", hint)
     dev = native.DeviceIndex(0)
@@ -152,3 +153,38 @@ def test_helped_sq8_768_spilled(native, sq8_setups, metric, ef):
                 rr = view.rerank(q, o_ids, 10, ef)
                 assert np.array_equal(r_ids[i], rr[0]) and np.array_equal(r_d[i].view(np.uint32), rr[1].view(np.uint32))
     assert memo > 0
+
+
+@pytest.mark.parametrize("ef", [12, 40])
+@pytest.mark.parametrize("metric", [1, 0])
+def test_helped_sq8_128_memo_over_the_table(native, orc, metric, ef):
+    """SQ8 d = 128 (AVX-512 order, spill table, helpers and the visited hint on by default): the
+    query region (512 B) is smaller than the memo (4 x 2 x 32 x 8 B), so the memo overlays the memo
+    wave's pool and visited table (memo_off > 0).  A wave that runs out of queries retires its
+    requests and sets its helper bit before it clears that area, and the hint's probe of a
+    sibling's wide table is bounded: batches of 1 .. 64 queries at small ef, where the
+    zeroed table would once have made a helper's probe spin, finish with the restatement's ids,
+    distance bits and counters."""
+    d, n = 128, 6000
+    rng = np.random.default_rng(910 + metric)
+    base = rng.standard_normal((n, d)).astype(np.float32)
+    queries = rng.standard_normal((64, d)).astype(np.float32)
+    g = native.Graph.build(base, metric, 32, 100, 8, 100)
+    mn, mx = native.sq8_train(base)
+    codes = native.sq8_encode(base, mn, mx, 8)
+    l0, levels, off, ue, ep, ur, _ = g.arrays()
+    view = orc.IndexView(base, l0, levels, off, ue, ur, ep, metric=metric, sq8=(codes, mn, mx, 2))
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, metric)
+    dev.set_graph(g)
+    dev.set_sq8(codes, mn, mx, 2)
+    dev.set_helpers(1)
+    for nq in (1, 5, 64):
+        qs = queries[:nq]
+        for rep in range(2):
+            s_ids, s_d, s_c = dev.search_sq8(qs, 10, ef, 0)
+            for i, q in enumerate(qs):
+                o_ids, o_d, o_c = view.search(q, 10, ef, with_counters=True)
+                assert np.array_equal(s_ids[i], o_ids), (nq, rep, i)
+                assert np.array_equal(s_d[i].view(np.uint32), o_d.view(np.uint32)), (nq, rep, i)
+                assert tuple(s_c[i]) == tuple(o_c), (nq, rep, i, s_c[i], o_c)
