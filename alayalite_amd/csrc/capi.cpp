@@ -116,6 +116,7 @@ struct alaya_index {
   DevBuf codes, sq_min, sq_max, rr_q_buf, sq_ids, sq_d;
   // flat path
   DevBuf norms, cand_d, cand_i, flat_tau, flag_buf, iota, flat_q;
+  int flat_contraction = -1;  // the last flat search's: 0 = f32, 1 = bf16 hi/lo split, 2 = single-pass f16
   bool norms_ready = false;
   float max_norm = 0.f;
   // scratch
@@ -619,9 +620,22 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
   p.norms = ix->norms.as<float>();
   p.valid = ix->has_valid ? ix->valid.as<uint32_t>() : nullptr;
   p.max_norm = ix->max_norm;
-  // bf16 split contraction unless the rows are large enough for bf16(x) to overflow, or
-  // ALAYA_FLAT_F32 is set (the f32-MFMA contraction; both feed the same exact rescoring)
-  p.split = ix->max_norm < 1e18f && std::getenv("ALAYA_FLAT_F32") == nullptr;
+  // The contraction that ranks the shortlist (all three feed the same exact rescoring and proof):
+  //  * single-pass f16 (default for rows of <= 224 floats, the warp-specialised scan): one MFMA per
+  //    16 k on power-of-two-scaled operands; needs the row scale 2^s in range (|s| <= 60);
+  //  * bf16 hi/lo split (wide rows, or rows out of the f16 scale's range, or
+  //    ALAYA_FLAT_CONTRACTION=bf16x3), unless the rows are large enough for bf16(x) to overflow;
+  //  * f32 MFMA (ALAYA_FLAT_CONTRACTION=f32 or ALAYA_FLAT_F32).
+  const char *fc = std::getenv("ALAYA_FLAT_CONTRACTION");
+  const std::string want = fc ? fc : (std::getenv("ALAYA_FLAT_F32") ? "f32" : "auto");
+  if (want != "auto" && want != "f16" && want != "bf16x3" && want != "f32")
+    throw ArgError("ALAYA_FLAT_CONTRACTION must be f16, bf16x3 or f32");
+  p.base_exp = alaya_amd::flat_base_exp(ix->max_norm);
+  const bool narrow = alaya_amd::flat_query_width(ix->stride) == 0;
+  p.single = (want == "auto" || want == "f16") && narrow && alaya_amd::flat_ws_available(0) &&
+             std::abs(p.base_exp) <= 60 && ix->max_norm > 0.f && std::isfinite(ix->max_norm);
+  p.split = !p.single && want != "f32" && ix->max_norm < 1e18f;
+  ix->flat_contraction = p.single ? 2 : (p.split ? 1 : 0);
   p.queries = d_q;
   p.nq = nq;
   p.q_stride = ix->dim;
@@ -1762,15 +1776,31 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
     alaya_amd::FlatParams p = flat_params(ix, ix->q_buf.as<float>(), nq, k, ix->id_buf.as<uint32_t>(),
                                           ix->dist_buf.as<float>(), ix->flag_buf.as<uint32_t>(), &blocks, ix->stream);
     flat_prescan(ix, p, &blocks, ix->stream);
-    hip_check(alaya_amd::launch_flat_scan(p, blocks, ix->stream), "flat scan");
-    hip_check(alaya_amd::launch_flat_merge(p, ix->stream), "flat merge");
-    scratch_release(ix, ix->stream);
     std::vector<uint32_t> flags(nq);
-    hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
     std::vector<float> dv(nq * k);
-    hip_check(hipMemcpyAsync(dv.data(), ix->dist_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
-    hip_check(hipMemcpyAsync(flags.data(), ix->flag_buf.ptr, nq * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
-    hip_check(hipStreamSynchronize(ix->stream), "flat search");
+    auto run = [&]() {
+      hip_check(alaya_amd::launch_flat_scan(p, blocks, ix->stream), "flat scan");
+      hip_check(alaya_amd::launch_flat_merge(p, ix->stream), "flat merge");
+      hip_check(hipMemcpyAsync(ids, ix->id_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+      hip_check(hipMemcpyAsync(dv.data(), ix->dist_buf.ptr, nq * k * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+      hip_check(hipMemcpyAsync(flags.data(), ix->flag_buf.ptr, nq * 4, hipMemcpyDeviceToHost, ix->stream), "D2H");
+      hip_check(hipStreamSynchronize(ix->stream), "flat search");
+    };
+    run();
+    if (p.single) {
+      // the single pass's bound is ~8x the split's: on data whose 10th and 32nd distances are that
+      // close, more than 1 % of the queries flagged reruns the launch with the bf16 hi/lo split
+      // before any exhaustive redo
+      uint64_t nflag = 0;
+      for (uint64_t q = 0; q < nq; ++q) nflag += flags[q] ? 1 : 0;
+      if (nflag * 100 > nq) {
+        p.single = 0;
+        p.split = ix->max_norm < 1e18f;
+        ix->flat_contraction = p.split ? 1 : 0;
+        run();
+      }
+    }
+    scratch_release(ix, ix->stream);
     // queries whose shortlist bound did not hold: exhaustive exact distances on the device, over
     // the valid rows only (the scan never returns a row cleared in the validity bitmap)
     uint32_t redo = 0;
@@ -1815,6 +1845,13 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
   });
 }
 
+int alaya_index_flat_last_contraction(const alaya_index *ix, int *contraction) {
+  return guarded([&] {
+    if (!ix || !contraction) throw ArgError("invalid arguments");
+    *contraction = ix->flat_contraction;
+  });
+}
+
 int alaya_index_set_hash_log2(alaya_index *ix, uint32_t log2_slots) {
   return guarded([&] {
     if (!ix) throw ArgError("null index");
@@ -1833,9 +1870,23 @@ int alaya_stream_create_reserving(int device, uint32_t reserved_cus, void **stre
     if (reserved_cus >= n) throw ArgError("reserved_cus must leave at least one CU");
     std::vector<uint32_t> mask((n + 31) / 32, 0u);
     for (uint32_t c = 0; c < n; ++c) mask[c / 32] |= 1u << (c % 32);
-    // the reserved CUs spread evenly over the CU numbering (so over the XCDs)
+    // The reserved CUs go one per XCD in turn.  Which XCD a CU-mask bit names is not documented
+    // (the bits may interleave, CU i on XCD i mod X, or run in blocks, CU i on XCD i / (n / X)), so
+    // reserved CU r is chosen on XCD r mod X under both numberings: c = x * (n / X) + ((x + X k) mod
+    // (n / X)) with x = r mod X, k = r / X (c mod X = x when X divides n / X).  A CU already taken
+    // (more than n / X reserved) moves to the next free one.
+    int xcds = 1;
+    if (hipDeviceGetAttribute(&xcds, hipDeviceAttributeNumberOfXccs, device) != hipSuccess || xcds < 1) {
+      (void)hipGetLastError();
+      xcds = 1;
+    }
+    const uint32_t X = static_cast<uint32_t>(xcds);
+    const uint32_t per = (n % X == 0) ? n / X : n;  // CUs per XCD (1 block when X does not divide n)
+    const uint32_t xs = (n % X == 0) ? X : 1u;
     for (uint32_t r = 0; r < reserved_cus; ++r) {
-      const uint32_t c = static_cast<uint32_t>((static_cast<uint64_t>(r) * n) / reserved_cus);
+      const uint32_t x = r % xs, k = r / xs;
+      uint32_t c = x * per + (x + xs * k) % per;
+      while (!(mask[c / 32] & (1u << (c % 32)))) c = (c + 1) % n;  // reserved_cus < n: a free CU exists
       mask[c / 32] &= ~(1u << (c % 32));
     }
     hipStream_t s = nullptr;

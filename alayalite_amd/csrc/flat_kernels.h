@@ -31,7 +31,10 @@ struct FlatParams {
   const float *tau_init;  // nq per-query starting thresholds (nullable = FLT_MAX): the prescan's
                           // 32nd-best over a row sample, nudged up one ulp (see flat_kernels.hip)
   float *tau_out;      // threshold kernel output (nq)
-  int split;           // 1 = bf16 hi/lo split contraction (3 bf16 MFMAs), 0 = f32 MFMA
+  int split;           // 1 = bf16 hi/lo split contraction (3 bf16 MFMAs), 0 = f32 MFMA (or single)
+  int single;          // 1 = single-pass f16 contraction (warp-specialised narrow scan only): rows scaled
+                       // by 2^base_exp, each query by its own power of two (flat_kernels.hip)
+  int base_exp;        // single pass: s with max|b| 2^s < 2^15 (flat_base_exp(max_norm))
   int ablate;          // diagnostics only: 1 = skip candidate handling (MFMA + tile stream only)
   uint32_t *merge_count;  // diagnostics only (nullable): merges per block
   uint32_t spin_limit; // warp-specialised scan: LDS-flag polls before a block aborts (its queries are
@@ -39,6 +42,10 @@ struct FlatParams {
 };
 
 int flat_shortlist();
+// whether the warp-specialised narrow scan runs (not the diagnostics' single-role kernel)
+bool flat_ws_available(int ablate);
+// the single pass's row scale exponent s for rows of largest norm max_norm (max|b| 2^s < 2^15)
+int flat_base_exp(float max_norm);
 // largest k of the flat path (merged list of 256 with a margin of 32)
 int flat_max_k();
 // slab width of the wide scan for rows of `stride` floats (0: the narrow kernel, stride <= 224)

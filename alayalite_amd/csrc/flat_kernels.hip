@@ -49,6 +49,26 @@ __device__ __forceinline__ void split_bf16(float x, __bf16 &hi, __bf16 &lo) {
   lo = static_cast<__bf16>(x - static_cast<float>(hi));
 }
 
+// Single-pass f16 contraction (FlatParams::single, the warp-specialised scan): one
+// v_mfma_f32_32x32x16_f16 per 16 k on operands scaled by powers of two into f16's range -- rows by
+// 2^s (base_exp, from the largest row norm: max|b| 2^s < 2^15), each query by its own 2^t (its
+// largest element, t = f16_exp(max|q|)) -- so C = 2^-(s+t) (q 2^t).(b 2^s) with exact scaling.
+// f16 keeps 11 significant bits: each operand is within 2^-11 relative (plus 2^-14 absolute, in
+// scaled units, should a tiny element flush to zero) of its f32 value, so the dropped terms are
+// bounded by ~2^-10 |q||b| (flat_merge_kernel's eps) -- 8x the split's bound, still far inside the
+// 10th-to-32nd distance gap of real data, at a third of the MFMAs and half the tile bytes.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr int kF16Top = 15;    // scaled operands stay below 2^15 (f16 max 65504)
+constexpr int kF16MaxExp = 100;  // |s + t| beyond this: the query is flagged (its scale-back leaves f32's range)
+// 2^t with |x| 2^t < 2^kF16Top for every |x| <= maxabs (0 for a zero or non-finite maxabs)
+__device__ __host__ __forceinline__ int f16_exp(float maxabs) {
+  if (!(maxabs > 0.f) || !(maxabs < 3.0e38f)) return 0;
+  int e = 0;
+  (void)frexpf(maxabs, &e);  // maxabs < 2^e
+  return kF16Top - e;
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ void wave_fence() {
@@ -517,16 +537,23 @@ __device__ __forceinline__ void lds_publish(uint32_t *a, uint32_t v) {
 
 // The consumer side of flat_scan_ws_kernel: wave `cw` of the pair w handles accumulator registers
 // [R0, R0 + NR) of its producer's tiles -- all 16 with one consumer per producer, 8 each with two.
-template <int kB, int kD, int kCons, int NR, int R0>
+template <int kB, int kD, int kCons, int NR, int R0, bool kOne>
 __device__ __forceinline__ void ws_consume(const FlatParams &p, const float *cx, uint32_t *published,
                                            uint32_t *consumed, uint32_t *abort, float *bd, uint32_t *bi, int w,
-                                           int half, uint64_t q0, int chunk, int ntiles, uint64_t r0, uint64_t r1) {
+                                           int half, uint64_t q0, int chunk, int ntiles, uint64_t r0, uint64_t r1,
+                                           const int *qexp) {
   const int lane = lane_id();
   const int h = lane >> 5;
   ShortlistsT<NR> S;
   init_shortlists<NR, R0>(p, q0, h, S);
   uint64_t t_app = 0, t_fold = 0;
   __syncthreads();
+  // single-pass f16: the contraction comes in scaled units; 2^-(s + t) per register's query (the
+  // producers wrote each query's t before the barrier)
+  f32xN<NR> unscale;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    unscale[r] = kOne ? ldexpf(1.0f, -(p.base_exp + qexp[w * 32 + reg_query(R0 + r, h)])) : 1.0f;
   const bool diag = p.merge_count != nullptr;
   uint64_t t_wait = 0;
   const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -552,6 +579,10 @@ __device__ __forceinline__ void ws_consume(const FlatParams &p, const float *cx,
 #pragma unroll
     for (int r = 0; r < NR; ++r) c[r] = in[r * 64];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's reads are done before it is released
+    if constexpr (kOne) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) c[r] *= unscale[r];  // a power of two: exact
+    }
     lds_publish(&consumed[w * kCons + half], static_cast<uint32_t>(t + 1));
     slot = slot + 1 == kD ? 0 : slot + 1;
     tile_candidates<kB, NR, R0>(p, c, bn, rid, live_mask, t == ntiles - 1, S, bd, bi, t_app, t_fold);
@@ -576,12 +607,14 @@ __device__ __forceinline__ void ws_consume(const FlatParams &p, const float *cx,
   store_shortlists<NR, R0>(p, q0, chunk, S);
 }
 
-template <int K, int kB, int kD, int kCons>
+// kOne: the single-pass f16 contraction (one MFMA per 16 k, an f16 tile); else the bf16 hi/lo split.
+template <int K, int kB, int kD, int kCons, bool kOne>
 __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatParams p) {
   static_assert(K % 16 == 0 && K <= 224, "narrow rows");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int kBPitch = K + 8;
-  constexpr int kTileWords = kTile * kBPitch;  // hi + lo bf16 half-tiles, 4-byte words per buffer
+  // 4-byte words per tile buffer: hi + lo bf16 half-tiles (split), one f16 tile (single pass)
+  constexpr int kTileWords = kOne ? kTile * kBPitch / 2 : kTile * kBPitch;
   float *tile = reinterpret_cast<float *>(smem);                   // 2 x kTileWords
   float *cx = tile + 2 * kTileWords;                                // kD x 4 waves x 16 regs x 64 lanes
   uint32_t *sync = reinterpret_cast<uint32_t *>(cx + kD * 4 * 16 * 64 + 4 * 32 * kB * 2);
@@ -589,6 +622,7 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
   uint32_t *consumed = sync + 4;             // [w * kCons + c]: tiles pair w's consumer c has read
   uint32_t *staged = sync + 4 + 4 * kCons;   // producer arrivals (4 per tile)
   uint32_t *abort = staged + 1;
+  int *qexp = reinterpret_cast<int *>(sync + 16);  // single pass: each query's scale exponent t (128)
   const int wave = threadIdx.x >> 6;
   const int w = wave & 3;
   const int lane = lane_id();
@@ -608,22 +642,46 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
 
   if (wave < 4) {
     // ---- producer ------------------------------------------------------------------------
-    bf16x8 ah[K / 16], al[K / 16];
+    bf16x8 ah[kOne ? 1 : K / 16], al[kOne ? 1 : K / 16];
+    f16x8 aq[kOne ? K / 16 : 1];
     {
       const uint64_t qi = q0 + col;
       const uint32_t e0 = h * (K / 2);
       const float *qp = p.queries + qi * p.q_stride;
+      if constexpr (kOne) {
+        // the query's scale 2^t from its largest element (both halves of the wave hold it)
+        float mx = 0.f;
 #pragma unroll
-      for (int s = 0; s < K / 16; ++s)
+        for (int s = 0; s < K / 16; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t e = e0 + 8 * s + j;
-          const float x = (qi < p.nq && e < p.dim) ? qp[e] : 0.f;
-          __bf16 hi, lo;
-          split_bf16(x, hi, lo);
-          ah[s][j] = hi;
-          al[s][j] = lo;
-        }
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t e = e0 + 8 * s + j;
+            mx = fmaxf(mx, fabsf((qi < p.nq && e < p.dim) ? qp[e] : 0.f));
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const int t = f16_exp(mx);
+        if (h == 0) qexp[w * 32 + col] = t;
+#pragma unroll
+        for (int s = 0; s < K / 16; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t e = e0 + 8 * s + j;
+            const float x = (qi < p.nq && e < p.dim) ? qp[e] : 0.f;
+            aq[s][j] = static_cast<_Float16>(ldexpf(x, t));
+          }
+      } else {
+#pragma unroll
+        for (int s = 0; s < K / 16; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t e = e0 + 8 * s + j;
+            const float x = (qi < p.nq && e < p.dim) ? qp[e] : 0.f;
+            __bf16 hi, lo;
+            split_bf16(x, hi, lo);
+            ah[s][j] = hi;
+            al[s][j] = lo;
+          }
+      }
     }
     constexpr int kVecPerRow = K / 4;
     constexpr int kVecs = kTile * kVecPerRow;
@@ -645,7 +703,15 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
 #pragma unroll
       for (int v = 0; v < kPerThread; ++v) {
         const int idx = threadIdx.x + v * 256;
-        if (idx < kVecs) {
+        if (idx < kVecs && kOne) {
+          _Float16 *th = reinterpret_cast<_Float16 *>(t) + (idx / kVecPerRow) * kBPitch + (idx % kVecPerRow) * 4;
+          f16x4 v4;
+          v4[0] = static_cast<_Float16>(ldexpf(reg[v].x, p.base_exp));
+          v4[1] = static_cast<_Float16>(ldexpf(reg[v].y, p.base_exp));
+          v4[2] = static_cast<_Float16>(ldexpf(reg[v].z, p.base_exp));
+          v4[3] = static_cast<_Float16>(ldexpf(reg[v].w, p.base_exp));
+          *reinterpret_cast<f16x4 *>(th) = v4;
+        } else if (idx < kVecs) {
           __bf16 *th = reinterpret_cast<__bf16 *>(t) + (idx / kVecPerRow) * kBPitch + (idx % kVecPerRow) * 4;
           bf16x4 hv, lv;
           __bf16 hi, lo;
@@ -678,14 +744,21 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
       if (kDeep && s + 2 < ntiles) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 2), ahead);
       if (!kDeep && s + 1 < ntiles) load_tile(r0 + static_cast<uint64_t>(kTile) * (s + 1), next);
       f32x16 c = {};
-      const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
+      if constexpr (kOne) {
+        const _Float16 *tq = reinterpret_cast<const _Float16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
 #pragma unroll
-      for (int st = 0; st < K / 16; ++st) {
-        const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * st);
-        const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * st);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[st], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c, 0, 0, 0);
+        for (int st = 0; st < K / 16; ++st)
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[st], *reinterpret_cast<const f16x8 *>(tq + 8 * st), c, 0, 0, 0);
+      } else {
+        const __bf16 *tb = reinterpret_cast<const __bf16 *>(tile + buf * kTileWords) + col * kBPitch + h * (K / 2);
+#pragma unroll
+        for (int st = 0; st < K / 16; ++st) {
+          const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(tb + 8 * st);
+          const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(tb + kTile * kBPitch + 8 * st);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[st], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[st], bh, c, 0, 0, 0);
+        }
       }
       // ring slot s % kD is free once the consumers have read tile s - kD
       const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -734,12 +807,15 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
     uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
     const int half = (wave - 4) / 4;
     if constexpr (kCons == 1) {
-      ws_consume<kB, kD, 1, 16, 0>(p, cx, published, consumed, abort, bd, bi, w, 0, q0, chunk, ntiles, r0, r1);
+      ws_consume<kB, kD, 1, 16, 0, kOne>(p, cx, published, consumed, abort, bd, bi, w, 0, q0, chunk, ntiles, r0, r1,
+                                         qexp);
     } else {
       if (half == 0)
-        ws_consume<kB, kD, 2, 8, 0>(p, cx, published, consumed, abort, bd, bi, w, 0, q0, chunk, ntiles, r0, r1);
+        ws_consume<kB, kD, 2, 8, 0, kOne>(p, cx, published, consumed, abort, bd, bi, w, 0, q0, chunk, ntiles, r0, r1,
+                                          qexp);
       else
-        ws_consume<kB, kD, 2, 8, 8>(p, cx, published, consumed, abort, bd, bi, w, 1, q0, chunk, ntiles, r0, r1);
+        ws_consume<kB, kD, 2, 8, 8, kOne>(p, cx, published, consumed, abort, bd, bi, w, 1, q0, chunk, ntiles, r0, r1,
+                                          qexp);
     }
   }
 }
@@ -977,6 +1053,37 @@ __device__ float exact_l2(const FlatParams &p, const float *q, uint32_t id, int 
   return res;
 }
 
+// The shortlist bound's slack on one query: rows outside the shortlist have true distance >=
+// cutoff + |q|^2 - eps, and the exact k-th result is within gam of its f32 value.  The shortlist
+// GEMM error is <= gam * (|q|^2 + max|b|^2 + 2|q| max|b|), gam = 2 k_acc u (u = 2^-24, conservative);
+// split contraction: the f32 accumulation covers 3K terms of total magnitude <= 1.02 |q||b|
+// (gam x 3.1), and the dropped terms (ql.bl and the two split residuals) add <= 3.02 * 2^-16 |q||b|
+// to C, i.e. twice that to the distance; 1e-30 covers bf16 lo parts flushed as denormals.
+// Single-pass f16 (operands scaled by 2^s, 2^t): every scaled operand is within 2^-11 relative plus
+// 2^-14 absolute (a flushed denormal) of its f32 value, so with a_b = 2^(-14-s), a_q = 2^(-14-t)
+// |C~ - C| <= (2^-10 + 2^-22) |q||b| + (1 + 2^-11) sqrt(K) (a_b |q| + a_q |b|) + K a_q a_b,
+// twice that on the distance (gam x 1.01 for the slightly larger rounded operands).  A query whose
+// scale-back 2^-(s+t) would leave f32's range is not provable: ok = false.
+__device__ __forceinline__ float shortlist_eps(const FlatParams &p, float qn, float qmax, float &gam, bool &ok) {
+  const float qnorm = sqrtf(qn);
+  const float bmax = p.max_norm;
+  ok = true;
+  gam = 2.0f * static_cast<float>(p.k_acc) * 5.9604645e-8f * (p.split ? 3.1f : (p.single ? 1.01f : 1.0f));
+  float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax);
+  if (p.single) {
+    const int t = f16_exp(qmax);
+    if (abs(p.base_exp + t) > kF16MaxExp || !(qn < 3.0e38f)) ok = false;
+    const float ab = ldexpf(1.0f, -14 - p.base_exp), aq = ldexpf(1.0f, -14 - t);
+    const float rk = sqrtf(static_cast<float>(p.k_acc));
+    const float ec = (9.7680283e-4f + 2.4e-7f) * qnorm * bmax + 1.0005f * rk * (ab * qnorm + aq * bmax) +
+                     static_cast<float>(p.k_acc) * aq * ab;
+    eps += 2.0f * 1.0001f * ec;
+  } else if (p.split) {
+    eps += 2.0f * 3.05f * 1.5258789e-5f * qnorm * bmax + 1e-30f;
+  }
+  return eps;
+}
+
 // One wave per query: merge the chunk shortlists (approximate distances), rescore the best kL
 // exactly, sort by (exact distance, id), emit k, flag the query if the bound does not hold.
 __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
@@ -989,13 +1096,17 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
   const int h = lane >> 5, col = lane & 31;
   for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
     const float *qs = p.queries + qi * p.q_stride;
-    float qn = 0.f;
+    float qn = 0.f, qmax = 0.f;
     for (uint32_t e = lane; e < p.stride; e += 64) {
       const float v = e < p.dim ? qs[e] : 0.f;
       q[e] = v;
       qn = fmaf(v, v, qn);
+      qmax = fmaxf(qmax, fabsf(v));
     }
-    for (int off = 32; off > 0; off >>= 1) qn += __shfl_xor(qn, off);
+    for (int off = 32; off > 0; off >>= 1) {
+      qn += __shfl_xor(qn, off);
+      qmax = fmaxf(qmax, __shfl_xor(qmax, off));
+    }
     // chunk shortlists (each ascending): half h folds chunks h, h+2, ...; then the halves swap
     float L = FLT_MAX;
     uint32_t Li = 0xffffffffu;
@@ -1047,24 +1158,16 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
       p.out_ids[qi * p.k + rank] = iv;
       if (p.out_dists) p.out_dists[qi * p.k + rank] = dv;
     }
-    // bound: rows outside the shortlist have true distance >= cutoff + |q|^2 - eps, where the
-    // shortlist GEMM error is <= gamma_K * (|q|^2 + max|b|^2 + 2|q| max|b|); the exact f32 value of
-    // the k-th result has relative error <= gamma_K.  gamma_K = 2 K u with u = 2^-24 (conservative).
+    // bound (shortlist_eps): rows outside the shortlist have true distance >= cutoff + |q|^2 - eps
     float kth_d = 0.f;
     {
       const uint64_t mk = __ballot(lane < kL && rank == p.k - 1);
       kth_d = mk ? __shfl(dv, __ffsll(static_cast<unsigned long long>(mk)) - 1) : FLT_MAX;
     }
-    // split contraction: the f32 accumulation covers 3K terms of total magnitude <= 1.02 |q||b|
-    // (gamma x 3.1), and the dropped terms (ql.bl and the two split residuals) add
-    // <= 3.02 * 2^-16 |q||b| to C, i.e. twice that to the distance; 1e-30 covers bf16 lo parts
-    // flushed as denormals.
-    const float gam = 2.0f * static_cast<float>(p.k_acc) * 5.9604645e-8f * (p.split ? 3.1f : 1.0f);
-    const float qnorm = sqrtf(qn);
-    const float bmax = p.max_norm;
-    const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax) +
-                      (p.split ? 2.0f * 3.05f * 1.5258789e-5f * qnorm * bmax + 1e-30f : 0.0f);
-    const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
+    float gam = 0.f;
+    bool ok = true;
+    const float eps = shortlist_eps(p, qn, qmax, gam, ok);
+    const bool exact = ok && (kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX);
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     wave_fence();
   }
@@ -1157,13 +1260,17 @@ __global__ void __launch_bounds__(64) flat_merge_big_kernel(FlatParams p) {
   const int lane = lane_id();
   for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
     const float *qs = p.queries + qi * p.q_stride;
-    float qn = 0.f;
+    float qn = 0.f, qmax = 0.f;
     for (uint32_t e = lane; e < p.stride; e += 64) {
       const float v = e < p.dim ? qs[e] : 0.f;
       q[e] = v;
       qn = fmaf(v, v, qn);
+      qmax = fmaxf(qmax, fabsf(v));
     }
-    for (int off = 32; off > 0; off >>= 1) qn += __shfl_xor(qn, off);
+    for (int off = 32; off > 0; off >>= 1) {
+      qn += __shfl_xor(qn, off);
+      qmax = fmaxf(qmax, __shfl_xor(qmax, off));
+    }
     VF<R> L;
     VU<R> Li;
 #pragma unroll
@@ -1223,12 +1330,10 @@ __global__ void __launch_bounds__(64) flat_merge_big_kernel(FlatParams p) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
       if ((p.k - 1) / 64 == static_cast<uint32_t>(r)) kth_d = __shfl(E[r], (p.k - 1) & 63);
-    const float gam = 2.0f * static_cast<float>(p.k_acc) * 5.9604645e-8f * (p.split ? 3.1f : 1.0f);
-    const float qnorm = sqrtf(qn);
-    const float bmax = p.max_norm;
-    const float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax) +
-                      (p.split ? 2.0f * 3.05f * 1.5258789e-5f * qnorm * bmax + 1e-30f : 0.0f);
-    const bool exact = kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX;
+    float gam = 0.f;
+    bool ok = true;
+    const float eps = shortlist_eps(p, qn, qmax, gam, ok);
+    const bool exact = ok && (kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX);
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1283,23 +1388,32 @@ size_t scan_lds() {
 
 template <int K>
 constexpr int ws_buf() { return 64; }  // consumer buffers shrink to fit 160 KB
-template <int K>
-constexpr int ws_ring() { return K <= 160 ? 3 : 2; }  // contraction slots per producer/consumer pair
+#ifndef ALAYA_FLAT_F16_RING
+#define ALAYA_FLAT_F16_RING 3  // diagnostics builds: ring slots of the single-pass scan
+#endif
+// contraction slots per producer/consumer pair (the single pass's half-size tile leaves room for more)
+template <int K, bool kOne = false>
+constexpr int ws_ring() { return kOne ? ALAYA_FLAT_F16_RING : (K <= 160 ? 3 : 2); }
 
-template <int K>
+// tile buffers (split: hi + lo bf16; single pass: one f16 tile), the ring, the candidate buffers, the
+// sync words and the queries' scale exponents
+template <int K, bool kOne = false>
 constexpr size_t ws_lds() {
-  return static_cast<size_t>(2 * kTile * (K + 8)) * 4 + ws_ring<K>() * 4 * 16 * 64 * 4 + 4 * (32 * ws_buf<K>() * 8) +
-         16 * 4;
+  return static_cast<size_t>(2 * kTile * (K + 8)) * (kOne ? 2 : 4) + ws_ring<K, kOne>() * 4 * 16 * 64 * 4 +
+         4 * (32 * ws_buf<K>() * 8) + 16 * 4 + 128 * 4;
 }
 // every narrow-row instantiation fits one block's 160 KB of LDS, and a candidate buffer holds a
 // whole tile of appends on top of the 32 a due fold leaves (tile_candidates' `need` rule)
-template <int K>
+template <int K, bool kOne = false>
 constexpr bool ws_fits() {
-  return ws_lds<K>() <= 160 * 1024 && ws_buf<K>() >= 2 * kTile;
+  return ws_lds<K, kOne>() <= 160 * 1024 && ws_buf<K>() >= 2 * kTile;
 }
 static_assert(ws_fits<32>() && ws_fits<64>() && ws_fits<96>() && ws_fits<128>() && ws_fits<160>() &&
                   ws_fits<192>() && ws_fits<224>(),
               "warp-specialised scan: LDS ring / candidate buffers");
+static_assert(ws_fits<32, true>() && ws_fits<64, true>() && ws_fits<96, true>() && ws_fits<128, true>() &&
+                  ws_fits<160, true>() && ws_fits<192, true>() && ws_fits<224, true>(),
+              "warp-specialised single-pass scan: LDS ring / candidate buffers");
 
 template <int KS>
 size_t wide_lds() {
@@ -1309,6 +1423,10 @@ size_t wide_lds() {
 }  // namespace
 
 int flat_shortlist() { return kL; }
+
+bool flat_ws_available(int ablate) { return ablate == 0 && std::getenv("ALAYA_FLAT_WS0") == nullptr; }
+
+int flat_base_exp(float max_norm) { return f16_exp(max_norm); }
 
 hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, float *norms, hipStream_t s) {
   if (n == 0) return hipSuccess;
@@ -1380,20 +1498,26 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
 #undef ALAYA_WIDE
     default: break;
   }
-  // the warp-specialised kernel for the split contraction; the single-role kernel for the f32
-  // contraction and the diagnostics (ablation, per-phase stamps)
-  const bool ws = p.split && p.ablate == 0 && std::getenv("ALAYA_FLAT_WS0") == nullptr;
+  // the warp-specialised kernel for the single-pass f16 and the split contraction; the single-role
+  // kernel for the f32 contraction and the diagnostics (ablation, per-phase stamps)
+  const bool ws = (p.split || p.single) && flat_ws_available(p.ablate);
   // two consumer waves per producer (default): config 2 566k -> 617k QPS (scan 1.76 -> 1.61 ms,
   // profiles/r04/flat/); ALAYA_FLAT_WS2=0 keeps one
   const char *ws2 = std::getenv("ALAYA_FLAT_WS2");
   const bool two = !(ws2 && ws2[0] == '0');
 #define ALAYA_FLAT(K)                                                                          \
   case K:                                                                                      \
-    if (ws && two)                                                                             \
-      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>(), 2>), dim3(blocks), dim3(768),    \
+    if (ws && p.single && two)                                                                 \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K, true>(), 2, true>), dim3(blocks), dim3(768), \
+                         (ws_lds<K, true>()), s, p);                                             \
+    else if (ws && p.single)                                                                   \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K, true>(), 1, true>), dim3(blocks), dim3(512), \
+                         (ws_lds<K, true>()), s, p);                                             \
+    else if (ws && two)                                                                        \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>(), 2, false>), dim3(blocks), dim3(768), \
                          ws_lds<K>(), s, p);                                                   \
     else if (ws)                                                                               \
-      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>(), 1>), dim3(blocks), dim3(512),    \
+      hipLaunchKernelGGL((flat_scan_ws_kernel<K, ws_buf<K>(), ws_ring<K>(), 1, false>), dim3(blocks), dim3(512), \
                          ws_lds<K>(), s, p);                                                   \
     else if (p.split)                                                                          \
       hipLaunchKernelGGL((flat_scan_kernel<K, true>), dim3(blocks), dim3(256), lds, s, p);     \

@@ -850,6 +850,11 @@ class DeviceIndex {
                                          reinterpret_cast<uint32_t *>(ids), reinterpret_cast<float *>(dists),
                                          reinterpret_cast<uint32_t *>(flags), reinterpret_cast<void *>(stream)));
   }
+  int flat_contraction() const {
+    int c = -1;
+    check(alaya_index_flat_last_contraction(ix_, &c));
+    return c;
+  }
   void flat_diag(uintptr_t q, uint64_t nq, uint32_t k, int ablate, uintptr_t ids, uintptr_t dists,
                  uintptr_t flags, uintptr_t mc, uintptr_t stream) {
     check(alaya_index_flat_diag(ix_, reinterpret_cast<const float *>(q), nq, k, ablate,
@@ -995,6 +1000,7 @@ PYBIND11_MODULE(_alayalitepy, m) {
       .def("flat_search", &DeviceIndex::flat_search, py::arg("queries"), py::arg("k"))
       .def("flat_search_device", &DeviceIndex::flat_search_device)
       .def("flat_diag", &DeviceIndex::flat_diag)
+      .def("flat_contraction", &DeviceIndex::flat_contraction)
       .def("search_sq8_device", &DeviceIndex::search_sq8_device)
       .def("shard_search_sq8_device", &DeviceIndex::shard_search_sq8_device)
       .def("set_sq8", &DeviceIndex::set_sq8, py::arg("codes"), py::arg("min"), py::arg("max"), py::arg("order") = 2)

@@ -294,6 +294,13 @@ __device__ __forceinline__ void query_end(const SearchParams &p, const Lds &L, c
 #ifndef ALAYA_HELP_DEPTH
 #define ALAYA_HELP_DEPTH 1
 #endif
+// Issue priority (s_setprio) of a searcher with helpers present: a helper shares its SIMD with up to
+// three waves of other workgroups, which may still be searching; the searchers' expansion chains run
+// at this priority and helpers at 0, so a helper's distance work fills issue slots the chains leave
+// free instead of delaying them.  0 = no priorities (diagnostics builds: -DALAYA_HELP_PRIO=0).
+#ifndef ALAYA_HELP_PRIO
+#define ALAYA_HELP_PRIO 2
+#endif
 constexpr int kHelpDepth = ALAYA_HELP_DEPTH;
 static_assert(kHelpDepth == 1 || kHelpDepth == 2, "help depth 1 or 2");
 constexpr int kHelpSlots = kHelpDepth + 1;  // requests per searcher
@@ -464,6 +471,7 @@ __device__ void help_siblings(const SearchParams &p, unsigned char *smem, const 
   const int lane = lane_id();
   const uint32_t R = p.R;
   const uint32_t full = (1u << W) - 1u;
+  if constexpr (ALAYA_HELP_PRIO > 0) __builtin_amdgcn_s_setprio(0);  // helpers yield to searchers
   // the visited hint (skip rows the sibling has already visited): by default where a stale read costs
   // a global round trip less than the rows it saves -- SQ8 on the spill table (config 5, 1k queries:
   // 3.47 ms with it, 3.62 without); the f32 rows of the SIFT shape are cheaper to compute than to
@@ -593,6 +601,7 @@ __global__ void __launch_bounds__(256)
   HelpBoard *board = kHelp ? help_board(p, smem, W) : nullptr;
   HelpMine mine;
   if constexpr (kHelp) {
+    if constexpr (ALAYA_HELP_PRIO > 0) __builtin_amdgcn_s_setprio(ALAYA_HELP_PRIO);
     if (threadIdx.x == 0) help_board_init(board);
     __syncthreads();
     for (int s = 0; s < kHelpSlots; ++s) mine.node[s] = kEmpty, mine.seq[s] = 0u;

@@ -364,7 +364,8 @@ def flat_scan_kernel_name(dim):
     contraction or the single-role scan is forced by environment."""
     if (dim + 31) // 32 * 32 > 224:
         return "flat_scan_wide_kernel"
-    if os.environ.get("ALAYA_FLAT_F32") or os.environ.get("ALAYA_FLAT_WS0"):
+    if (os.environ.get("ALAYA_FLAT_F32") or os.environ.get("ALAYA_FLAT_WS0")
+            or os.environ.get("ALAYA_FLAT_CONTRACTION") == "f32"):
         return "flat_scan_kernel"
     return "flat_scan_ws_kernel"
 
@@ -423,11 +424,12 @@ def run_flat(args):
     flops = 2.0 * n * nq * dim
     tf = flops / (ms * 1e-3) / 1e12
     scan = flat_scan_kernel_name(dim)
-    # the roofline is the issued contraction's own MFMA peak: the default bf16 hi/lo split issues 3
-    # bf16 products per f32 product, so its ceiling is the dense bf16 peak (16 x 157.3 TF) / 3; the f32
-    # contraction (ALAYA_FLAT_F32) runs at the 157.3 TF f32 MFMA peak
-    f32_contraction = bool(os.environ.get("ALAYA_FLAT_F32"))
-    mfma_peak = 157.3 if f32_contraction else round(16 * 157.3 / 3, 1)
+    # the roofline is the issued contraction's own MFMA peak (alaya_index_flat_last_contraction):
+    # the single-pass f16 (default for rows of <= 224 floats) issues one f16 product per f32 product,
+    # so its ceiling is the dense f16 peak (16 x 157.3 TF); the bf16 hi/lo split issues 3 bf16
+    # products per f32 product (dense bf16 peak / 3); the f32 contraction runs at the 157.3 TF f32 peak
+    contraction = {0: "f32", 1: "bf16x3", 2: "f16"}[index.flat_contraction()]
+    mfma_peak = {"f32": 157.3, "bf16x3": round(16 * 157.3 / 3, 1), "f16": round(16 * 157.3, 1)}[contraction]
     # HBM traffic of the scan from the committed PMC passes on this workload and kernel
     # (tools/run_pmc_flat.sh; latest round first)
     import glob
@@ -436,7 +438,8 @@ def run_flat(args):
     for tpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_flat*.json")), reverse=True):
         t = json.load(open(tpath))
         c = t.get("config", {})
-        if (c.get("n_base"), c.get("n_queries"), c.get("dim"), t.get("kernel")) == (n, nq, dim, scan):
+        if ((c.get("n_base"), c.get("n_queries"), c.get("dim"), t.get("kernel"), t.get("contraction", "bf16x3"))
+                == (n, nq, dim, scan, contraction)):
             traffic, tsrc = t, os.path.relpath(tpath, ROOT)
             break
     cpu = None
@@ -471,11 +474,13 @@ def run_flat(args):
                      "kernel": f"{scan}+flat_merge_kernel",
                      "kernel_ms": round(ms, 4), "algorithmic_flops_per_launch": flops,
                      # achieved = algorithmic f32 products (2 n nq d) / kernel time; peak = the issued
-                     # contraction's dense MFMA peak (bf16x3: 2516.8 TF / 3; f32: 157.3 TF)
-                     "contraction": "f32" if f32_contraction else "bf16x3",
-                     "peak_source": ("f32 MFMA dense peak (MI355X_MICROARCH.md)" if f32_contraction else
-                                     "bf16 MFMA dense peak 16 x 157.3 TF / 3 bf16 products per f32 product "
-                                     "(MI355X_MICROARCH.md)")},
+                     # contraction's dense MFMA peak (f16: 2516.8 TF; bf16x3: 2516.8 TF / 3; f32: 157.3 TF)
+                     "contraction": contraction,
+                     "peak_source": {"f32": "f32 MFMA dense peak (MI355X_MICROARCH.md)",
+                                     "bf16x3": "bf16 MFMA dense peak 16 x 157.3 TF / 3 bf16 products per f32 "
+                                               "product (MI355X_MICROARCH.md)",
+                                     "f16": "f16 MFMA dense peak 16 x 157.3 TF, one f16 product per f32 product "
+                                            "(MI355X_MICROARCH.md)"}[contraction]},
         "cpu_baseline": cpu,
         "build": _native.build_provenance(),
     }
@@ -797,6 +802,17 @@ def main():
         cpu = cpu_baseline(args, graph, base, queries, ef, metric, sq8, ids_dev.cpu().numpy().astype(np.uint32))
         log("cpu baseline", cpu)
 
+    # ---- memory per rank: the N-rank command sized against one node's host memory and HBM ----------
+    import resource
+
+    free_b, total_b = torch.cuda.mem_get_info(dev)
+    mem = {"rank": rank, "host_peak_rss_gb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2),
+           "device_used_gb": round((total_b - free_b) / 2**30, 2)}
+    mems = [mem]
+    if world > 1:
+        mems = [None] * world
+        dist.all_gather_object(mems, mem)
+
     if rank == 0:
         r_at = next((s["recall"] for s in sweep if s["ef"] == ef), None)
         out = {
@@ -844,6 +860,10 @@ def main():
             "cpu_baseline": cpu,
             # which sources the loaded libalaya_hip.so was compiled from, against this tree's
             "build": _native.build_provenance(),
+            "memory": {"per_rank": mems,
+                       "note": "host_peak_rss_gb: the rank's peak resident set (getrusage); device_used_gb: "
+                               "memory in use on the rank's GPU at the end of the run (hipMemGetInfo: every "
+                               "process on that GPU, so all ranks when a rehearsal shares one GPU)"},
         }
         if curve is not None:
             out["config"]["qps_curve"] = curve

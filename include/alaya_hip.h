@@ -212,9 +212,11 @@ int alaya_index_shard_search_sq8_device(alaya_index *ix, const float *d_queries,
 /* ---- flat (exhaustive) exact k-NN, L2, any dim, 1 <= k <= 224 -----------------------------------
  * No reference implementation (IndexType::FLAT is enum-only, include/index/index_type.hpp:28); the
  * analogue is find_exact_gt (include/utils/evaluate.hpp:29-62).  An MFMA pass ranks every row
- * by |b|^2 - 2 q.b and keeps a shortlist -- by default q.b from a bf16 hi/lo split (3 bf16 MFMAs,
- * error bounded and folded into the proof below); environment ALAYA_FLAT_F32=1 selects the f32
- * MFMA form; rows wider than 224 floats are scanned in K slabs.  The shortlist (32 per row chunk,
+ * by |b|^2 - 2 q.b and keeps a shortlist -- q.b from a single-pass f16 contraction on power-of-two
+ * scaled operands (rows of <= 224 floats) or a bf16 hi/lo split (3 bf16 MFMAs; wider rows), each
+ * error bounded and folded into the proof below (alaya_index_flat_last_contraction; environment
+ * ALAYA_FLAT_CONTRACTION selects one, ALAYA_FLAT_F32=1 the f32 MFMA form); rows wider than 224
+ * floats are scanned in K slabs.  The shortlist (32 per row chunk,
  * folded into a 128/256-entry list for k > 24) is rescored with the exact device metric
  * (l2_sqr_avx2 order) and sorted by (distance, id).  A query whose shortlist cannot be proven to
  * hold the exact top-k (error bound in flat_kernels.hip) is flagged; the host API recomputes it
@@ -225,6 +227,13 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
                             uint32_t *ids, float *dists, uint32_t *n_recomputed);
 int alaya_index_flat_search_device(alaya_index *ix, const float *d_queries, uint64_t nq, uint32_t k,
                                    uint32_t *d_ids, float *d_dists, uint32_t *d_flags, void *stream);
+/* The contraction the last flat search ranked its shortlist with (introspection): 2 = single-pass f16
+ * (the default for rows of <= 224 floats: one f16 MFMA per 16 k on operands scaled by powers of two,
+ * error bound ~2^-10 |q||b|; the host API reruns a launch with the split if more than 1 % of its
+ * queries are flagged), 1 = bf16 hi/lo split (3 bf16 MFMAs; wide rows and out-of-range scales),
+ * 0 = f32 MFMA; -1 before any flat search.  Environment ALAYA_FLAT_CONTRACTION = f16 | bf16x3 | f32
+ * selects one. */
+int alaya_index_flat_last_contraction(const alaya_index *ix, int *contraction);
 /* Tuning / introspection: LDS visited-table size (log2 slots, 6..16; 0 = automatic) and layout
  * (0 = automatic, 1 = compact 16-bit slots, 2 = 32-bit id slots, 3 = compact with probe distance
  * capped at 2, a test hook for the spill-on-long-probe path).  Results never depend on either:

