@@ -1389,9 +1389,10 @@ size_t scan_lds() {
 template <int K>
 constexpr int ws_buf() { return 64; }  // consumer buffers shrink to fit 160 KB
 #ifndef ALAYA_FLAT_F16_RING
-#define ALAYA_FLAT_F16_RING 3  // diagnostics builds: ring slots of the single-pass scan
+#define ALAYA_FLAT_F16_RING 4  // diagnostics builds: ring slots of the single-pass scan
 #endif
-// contraction slots per producer/consumer pair (the single pass's half-size tile leaves room for more)
+// contraction slots per producer/consumer pair (the single pass's half-size tile leaves room for more:
+// 4 slots against 3, config 2 1.301 -> 1.267 ms, profiles/r06/flat/ab_ring_*.log)
 template <int K, bool kOne = false>
 constexpr int ws_ring() { return kOne ? ALAYA_FLAT_F16_RING : (K <= 160 ? 3 : 2); }
 

@@ -14,6 +14,15 @@
 #   rehearse8   the driver's N = 8 command at its defaults (config 4) with every rank on cuda:0 over gloo
 #   rehearse8-sq8
 #               N = 8 on the config-5 workload at N8_ROWS rows (default 2M), every rank on cuda:0
+#   shard-rehearsal <gist|sq8>
+#               tools/shard_rehearsal.py at config 4's / config 5's batch: every layout's shard graphs
+#               built and timed on one GPU, the predicted N = 8 efficiencies
+#   build-quality
+#               the device HNSW build's tests, recall of the device graph vs the host builder at 1M
+#               (tools/build_quality.py) and a rocprofv3 summary of the build kernels
+#   graph-quality
+#               the device-built graph's recall@10-vs-ef curve on the headline data (tools/graph_quality.py;
+#               its host single-thread counterpart runs on the CPU)
 #   ab-flat "v1 v2 ..."
 #               config 2's flat scan timed per variant (tools/ab_flat.py; "tree" = this tree's build,
 #               anything else = a saved build ab/<name>, tools/build_ab.sh), interleaved twice
@@ -90,6 +99,24 @@ case "$recipe" in
     step 1150 gpurun_out/${P}_rehearse8_c5.log python -u bench.py --gpus 8 --workload sq8-ip --n "${N8_ROWS:-2000000}"
     echo "wall_s=$(( $(date +%s) - t0 ))" | tee gpurun_out/${P}_rehearse8_c5.wall
     json gpurun_out/${P}_rehearse8_c5.log
+    ;;
+  shard-rehearsal)
+    wl=${3:-gist}
+    step 900 gpurun_out/${P}_shard_rehearsal_$wl.log python -u tools/shard_rehearsal.py --workload "$wl" --nq 10000 \
+      --out gpurun_out/${P}_shard_rehearsal_${wl}_10k.json
+    ;;
+  build-quality)
+    step 300 gpurun_out/${P}_gpu_build_tests.log python -u -m pytest tests/test_gpu_build.py -x -q -p no:cacheprovider \
+      --timeout 120 --timeout-method thread
+    step 600 gpurun_out/${P}_bq_1m.log python -u tools/build_quality.py --n 1000000 --host
+    step 400 gpurun_out/${P}_bq_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${P}_build -o run \
+      --output-format csv -- python -u tools/build_quality.py --n 1000000 --efs 400
+    find gpurun_out/prof_${P}_build -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/${P}_build_kernel_stats.csv
+    rm -rf gpurun_out/prof_${P}_build
+    ;;
+  graph-quality)
+    step 600 gpurun_out/${P}_graph_quality_device.log python -u tools/graph_quality.py --graph device \
+      --out gpurun_out/${P}_graph_quality_device_gist1m.json
     ;;
   ab-flat)
     for rep in 1 2; do
