@@ -13,7 +13,7 @@
 #               HBM traffic (PMC passes, tools/run_pmc.sh / run_pmc_flat.sh) at the config's operating point
 #   rehearse8   the driver's N = 8 command at its defaults (config 4) with every rank on cuda:0 over gloo
 #   rehearse8-sq8
-#               N = 8 on the config-5 workload at N8_ROWS rows (default 2M), every rank on cuda:0
+#               N = 8 on the config-5 workload at N8_ROWS rows (default 4M) and N8_NQ queries (default 10k), every rank on cuda:0
 #   shard-rehearsal <gist|sq8>
 #               tools/shard_rehearsal.py at config 4's / config 5's batch: every layout's shard graphs
 #               built and timed on one GPU, the predicted N = 8 efficiencies
@@ -96,7 +96,7 @@ case "$recipe" in
   rehearse8-sq8)
     export ALAYA_BENCH_REHEARSE=1
     t0=$(date +%s)
-    step 1150 gpurun_out/${P}_rehearse8_c5.log python -u bench.py --gpus 8 --workload sq8-ip --n "${N8_ROWS:-2000000}"
+    step 1150 gpurun_out/${P}_rehearse8_c5.log python -u bench.py --gpus 8 --workload sq8-ip --n "${N8_ROWS:-4000000}" --nq "${N8_NQ:-10000}"
     echo "wall_s=$(( $(date +%s) - t0 ))" | tee gpurun_out/${P}_rehearse8_c5.wall
     json gpurun_out/${P}_rehearse8_c5.log
     ;;
