@@ -363,7 +363,7 @@ uint32_t size_visited(alaya_index *ix, SearchParams &p, uint64_t nq, uint32_t ef
   }
   const size_t shared = alaya_amd::search_shared_lds_bytes(ix->stride, p.sq8_order != 0) +
                         (p.help ? alaya_amd::kHelpBoardBytes : 0);
-  const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0) - 4;
+  const size_t wave_fixed = alaya_amd::search_wave_lds_bytes(ix->stride, ef, 0, false, p.sq8_order) - 4;
   // the register-bound residency, probed with a 4 KB table.  The 1 KB probe applies only to the
   // forced compact modes (1, 3) with a spill table: every other mode with a spill table returned
   // set_mode(7) above.
@@ -500,14 +500,15 @@ void do_search(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint3
     while (!p.help && W > 1 && static_cast<uint64_t>(W) > nq) W /= 2;
     p.hash_log2 = size_visited(ix, p, nq, ef, W);
     const bool compact = p.vis_rbits != alaya_amd::kVisWide;
-    p.wave_lds = static_cast<uint32_t>(alaya_amd::search_wave_lds_bytes(ix->stride, ef, p.hash_log2, compact));
+    p.wave_lds = static_cast<uint32_t>(alaya_amd::search_wave_lds_bytes(ix->stride, ef, p.hash_log2, compact,
+                                                                        p.sq8_order));
     bool fits = true;
     if (p.help) {
       // the memo (W searchers x kHelpMemoSlots requests x R entries of 8 bytes) overlays the memo
       // wave's query vector, or else its pool and visited table (past the query and the three
       // 64-entry lists the helper still uses)
       const size_t need = static_cast<size_t>(W) * alaya_amd::kHelpMemoSlots * ix->R * 8;
-      const size_t q_bytes = static_cast<size_t>(ix->stride) * 4;
+      const size_t q_bytes = alaya_amd::search_query_lds_bytes(ix->stride, p.sq8_order);
       if (q_bytes >= need) {
         p.memo_off = 0;
       } else if (p.wave_lds >= q_bytes + 3 * 64 * 4 + need) {

@@ -344,13 +344,42 @@ __device__ __forceinline__ float sq8_term(float xq, float scale, float mn, float
   return fmaf(d, d, acc);
 }
 
-template <bool kIP>
+// The query's term per dimension: x = float(code) (L2) or xv = fma(float(code), scale, min) (IP), read
+// from LDS as f32 (kCodes = false), or rebuilt from the query's one-byte codes (kCodes: the
+// AVX-512-order kernels with ALAYA_SQ8_QCODES, a quarter of the LDS) with the same operations as the
+// encoder, so the value -- and every distance -- is bit-identical.
+#ifndef ALAYA_SQ8_QCODES
+#define ALAYA_SQ8_QCODES 0
+#endif
+template <int kOrder>
+constexpr bool sq8_query_codes() { return ALAYA_SQ8_QCODES != 0 && kOrder == 2; }
+
+template <bool kIP, bool kCodes>
+__device__ __forceinline__ float4 sq8_qterm4(const float *xq, const float4 &s, const float4 &mn, int e) {
+  if constexpr (!kCodes) {
+    return *reinterpret_cast<const float4 *>(xq + e);
+  } else {
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(xq) + e);
+    const float c0 = static_cast<float>(w & 0xffu), c1 = static_cast<float>((w >> 8) & 0xffu);
+    const float c2 = static_cast<float>((w >> 16) & 0xffu), c3 = static_cast<float>(w >> 24);
+    if (kIP) return make_float4(fmaf(c0, s.x, mn.x), fmaf(c1, s.y, mn.y), fmaf(c2, s.z, mn.z), fmaf(c3, s.w, mn.w));
+    return make_float4(c0, c1, c2, c3);
+  }
+}
+template <bool kIP, bool kCodes>
+__device__ __forceinline__ float sq8_qterm(const float *xq, const float *sc, const float *mnv, int e) {
+  if constexpr (!kCodes) return xq[e];
+  const float c = static_cast<float>(reinterpret_cast<const uint8_t *>(xq)[e]);
+  return kIP ? fmaf(c, sc[e], mnv[e]) : c;
+}
+
+template <bool kIP, bool kCodes = false>
 __device__ __forceinline__ void sq8_chunk(const float *xq, const float *sc, const float *mnv, int e,
                                           uint32_t w, float *acc) {
-  const float4 x = *reinterpret_cast<const float4 *>(xq + e);
   const float4 s = *reinterpret_cast<const float4 *>(sc + e);
   float4 mn = make_float4(0.f, 0.f, 0.f, 0.f);
   if (kIP) mn = *reinterpret_cast<const float4 *>(mnv + e);
+  const float4 x = sq8_qterm4<kIP, kCodes>(xq, s, mn, e);
   acc[0] = sq8_term<kIP>(x.x, s.x, mn.x, static_cast<float>(w & 0xffu), acc[0]);
   acc[1] = sq8_term<kIP>(x.y, s.y, mn.y, static_cast<float>((w >> 8) & 0xffu), acc[1]);
   acc[2] = sq8_term<kIP>(x.z, s.z, mn.z, static_cast<float>((w >> 16) & 0xffu), acc[2]);
@@ -433,6 +462,7 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
   // the AVX2 order keeps it, because without it the compiler schedules the 48-chunk loop into
   // 186-235 VGPRs (2 waves per SIMD) instead of 121-144.
   constexpr bool kTail = kOrder == 1;
+  constexpr bool kCodes = sq8_query_codes<kOrder>();
   const int rem = kTail ? static_cast<int>(p.dim) - P * kFull : 0;
   const bool half = kTail && rem >= P / 2;
   const int tail_begin = P * kFull + (half ? P / 2 : 0);
@@ -454,10 +484,10 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
     __builtin_amdgcn_sched_barrier(0);
 #endif
     const int e = P * t + 4 * m;
-    const float4 x = *reinterpret_cast<const float4 *>(xq + e);
     const float4 s = *reinterpret_cast<const float4 *>(sc + e);
     float4 mn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (kIP) mn = *reinterpret_cast<const float4 *>(mnv + e);
+    const float4 x = sq8_qterm4<kIP, kCodes>(xq, s, mn, e);
 #pragma unroll
     for (int r = 0; r < SP::kR; ++r) {
       if (r >= live) break;
@@ -474,8 +504,8 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
     if (r >= live) break;
     const uint8_t *rw = p.codes + static_cast<uint64_t>(S.id[r]) * p.code_stride;
     if (half && m < LPR / 2 && S.act[r])  // trailing half block -> acc[0 .. P/2)
-      sq8_chunk<kIP>(xq, sc, mnv, P * kFull + 4 * m, *reinterpret_cast<const uint32_t *>(rw + P * kFull + 4 * m),
-                     acc[r]);
+      sq8_chunk<kIP, kCodes>(xq, sc, mnv, P * kFull + 4 * m,
+                             *reinterpret_cast<const uint32_t *>(rw + P * kFull + 4 * m), acc[r]);
     float a0 = acc[r][0], a1 = acc[r][1], a2 = acc[r][2], a3 = acc[r][3];
     if constexpr (kOrder == 2) {
       a0 += lane_xor<4>(a0); a1 += lane_xor<4>(a1); a2 += lane_xor<4>(a2); a3 += lane_xor<4>(a3);
@@ -486,7 +516,7 @@ __device__ __forceinline__ void sq8_finish(const SearchParams &p, const float *x
     if (S.act[r] && m == 0) {
       if constexpr (kTail) {
         for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
-          res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(rw[e]), res);
+          res = sq8_term<kIP>(sq8_qterm<kIP, kCodes>(xq, sc, mnv, e), sc[e], mnv[e], static_cast<float>(rw[e]), res);
       }
       out[base + g + G * r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
     }
@@ -507,6 +537,7 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
   constexpr int LPR = P / 4;    // lanes per row
   constexpr int G = 64 / LPR;   // row groups per wave
   constexpr int kRPL = sq8_rows_per_group<kOrder, kFull>();
+  constexpr bool kCodes = sq8_query_codes<kOrder>();
   if constexpr (kFull > 0) {
     for (int base = 0; base < n; base += G * kRPL) {
       Sq8Pass<kOrder, kFull> S;
@@ -551,21 +582,21 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
       for (int r = 0; r < kRPL; ++r) {
         if (base + G * r >= n) break;
 #pragma unroll
-        for (int t = 0; t < kFull; ++t) sq8_chunk<kIP>(xq, sc, mnv, P * t + 4 * m, w[r][t], acc[r]);
+        for (int t = 0; t < kFull; ++t) sq8_chunk<kIP, kCodes>(xq, sc, mnv, P * t + 4 * m, w[r][t], acc[r]);
       }
     } else {
       if (act[0]) {
         for (int t = 0; t < T; ++t)
-          sq8_chunk<kIP>(xq, sc, mnv, P * t + 4 * m, *reinterpret_cast<const uint32_t *>(row[0] + P * t + 4 * m),
-                         acc[0]);
+          sq8_chunk<kIP, kCodes>(xq, sc, mnv, P * t + 4 * m,
+                                 *reinterpret_cast<const uint32_t *>(row[0] + P * t + 4 * m), acc[0]);
       }
     }
 #pragma unroll
     for (int r = 0; r < kRPL; ++r) {
       if (base + G * r >= n) break;
       if (half && m < LPR / 2 && act[r])  // trailing half block -> acc[0 .. P/2)
-        sq8_chunk<kIP>(xq, sc, mnv, P * T + 4 * m, *reinterpret_cast<const uint32_t *>(row[r] + P * T + 4 * m),
-                       acc[r]);
+        sq8_chunk<kIP, kCodes>(xq, sc, mnv, P * T + 4 * m, *reinterpret_cast<const uint32_t *>(row[r] + P * T + 4 * m),
+                               acc[r]);
       float a0 = acc[r][0], a1 = acc[r][1], a2 = acc[r][2], a3 = acc[r][3];
       if constexpr (kOrder == 2) {  // a = sum0 + sum1 (lanes m, m+4)
         a0 += lane_xor<4>(a0); a1 += lane_xor<4>(a1); a2 += lane_xor<4>(a2); a3 += lane_xor<4>(a3);
@@ -578,7 +609,7 @@ __device__ __forceinline__ void sq8_distances(const SearchParams &p, const float
       if (act[r] && m == 0) {
         const uint8_t *rw = row[r];
         for (int e = tail_begin; e < static_cast<int>(p.dim); ++e)
-          res = sq8_term<kIP>(xq[e], sc[e], mnv[e], static_cast<float>(rw[e]), res);
+          res = sq8_term<kIP>(sq8_qterm<kIP, kCodes>(xq, sc, mnv, e), sc[e], mnv[e], static_cast<float>(rw[e]), res);
         out[base + g + G * r] = kIP ? -res : res;  // no validity check in SQ8Space::QueryComputer
       }
     }

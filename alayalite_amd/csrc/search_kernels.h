@@ -116,7 +116,11 @@ constexpr uint32_t kStabBucket = 8;  // spill-table entries per bucket (16 B: on
 inline size_t visited_table_bytes(uint32_t hash_log2, bool compact) {
   return (static_cast<size_t>(compact ? 2 : 4)) << hash_log2;
 }
-size_t search_wave_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact = false);
+size_t search_wave_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact = false,
+                             int sq8_order = 0);
+// bytes of a wave's query region: stride f32 terms, or the query's codes (AVX-512-order SQ8 kernels
+// built with ALAYA_SQ8_QCODES)
+size_t search_query_lds_bytes(uint32_t stride, int sq8_order);
 __host__ __device__ inline size_t search_shared_lds_bytes(uint32_t stride, bool sq8) {
   return sq8 ? 2 * static_cast<size_t>(stride) * 4 : 0;
 }

@@ -70,7 +70,7 @@ __device__ __forceinline__ Lds carve_lds(const SearchParams &p, unsigned char *s
   Lds L;
   unsigned char *ptr = smem + search_shared_lds_bytes(p.stride, space_sq8<kSpace>()) + static_cast<size_t>(wave) * p.wave_lds;
   L.q = reinterpret_cast<float *>(ptr);
-  ptr += static_cast<size_t>(p.stride) * 4;
+  ptr += sq8_query_codes<kSpace>() ? (static_cast<size_t>(p.stride) + 15) / 16 * 16 : static_cast<size_t>(p.stride) * 4;
   L.cid = reinterpret_cast<uint32_t *>(ptr);
   ptr += 64 * 4;
   L.cd = reinterpret_cast<float *>(ptr);
@@ -124,11 +124,11 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
     // (the per-index scale and min are the workgroup's shared LDS copy, fill_shared)
     for (uint32_t e = lane; e < p.stride; e += 64) {
       float xq = 0.f;
+      uint32_t code = 0;
       if (e < p.dim) {
         const float v = qsrc[e];
         const float mn = p.sq_min[e];
         const float mx = p.sq_max[e];
-        uint32_t code;
         if (mx == mn) code = 0;
         else if (v >= mx) code = 255;
         else if (v <= mn) code = 0;
@@ -136,7 +136,11 @@ __device__ __forceinline__ void query_begin(const SearchParams &p, const Lds &L,
         const float xf = static_cast<float>(code);
         xq = kIP ? fmaf(xf, L.sq_scale[e], mn) : xf;
       }
-      L.q[e] = xq;
+      if constexpr (sq8_query_codes<kSpace>()) {
+        reinterpret_cast<uint8_t *>(L.q)[e] = static_cast<uint8_t>(code);  // the term is rebuilt per chunk
+      } else {
+        L.q[e] = xq;
+      }
     }
   }
   {
@@ -982,8 +986,14 @@ hipError_t launch_stream_read(const void *buf, uint64_t bytes, int grid, int sha
   return hipGetLastError();
 }
 
-size_t search_wave_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact) {
-  return static_cast<size_t>(stride) * 4 + 3 * 64 * 4 + 2 * (((ef + 1) * 4 + 15) / 16 * 16) +
+size_t search_query_lds_bytes(uint32_t stride, int sq8_order) {
+  // the query as f32 terms, or (ALAYA_SQ8_QCODES, AVX-512-order SQ8) as its codes, 16 B aligned
+  return sq8_order == 2 && sq8_query_codes<2>() ? (static_cast<size_t>(stride) + 15) / 16 * 16
+                                                : static_cast<size_t>(stride) * 4;
+}
+
+size_t search_wave_lds_bytes(uint32_t stride, uint32_t ef, uint32_t hash_log2, bool compact, int sq8_order) {
+  return search_query_lds_bytes(stride, sq8_order) + 3 * 64 * 4 + 2 * (((ef + 1) * 4 + 15) / 16 * 16) +
          visited_table_bytes(hash_log2, compact);
 }
 
