@@ -118,6 +118,11 @@ struct alaya_index {
   DevBuf norms, cand_d, cand_i, flat_tau, flag_buf, iota, flat_q;
   int flat_contraction = -1;  // the last flat search's: 0 = f32, 1 = bf16 hi/lo split, 2 = single-pass f16
   bool norms_ready = false;
+  // single-role f16 flat scan: the base's tile records (alaya_amd::launch_flat_tiles), built at the
+  // first flat search after any change to the rows, their count or the validity bitmap
+  DevBuf flat_tiles;
+  bool tiles_ready = false;
+  int tiles_exp = 0;
   float max_norm = 0.f;
   // scratch
   DevBuf work, overflow, dirty, stab, q_buf, id_buf, dist_buf, cnt_buf, dlist_buf, dout_buf;
@@ -573,6 +578,40 @@ int flat_chunks(alaya_index *ix, int nqg, uint64_t rows) {
   return static_cast<int>(std::min<uint64_t>(chunks, max_chunks));
 }
 
+// Chunks per query group of the single-role f16 scan (256 queries per block, one block per CU): the
+// fewest chunks that give every CU a block; past that, the chunk count in 8..64 whose blocks fill
+// whole rounds of the CUs best (fewer chunks on ties -- each chunk adds ~32 ln(rows) appends per
+// query).  Every chunk keeps >= 4 records.
+int flat_tiles_chunks(alaya_index *ix, uint64_t nq, uint64_t scan_tiles) {
+  const uint64_t nqg = (nq + alaya_amd::flat_tiles_queries() - 1) / alaya_amd::flat_tiles_queries();
+  const uint64_t cus = static_cast<uint64_t>(std::max(1, ix->num_cus));
+  const uint64_t cap = std::max<uint64_t>(8, std::min<uint64_t>(256, (scan_tiles / 4) / 8 * 8));
+  if (nqg * 8 < cus) return static_cast<int>(std::min<uint64_t>(cap, (cus + nqg - 1) / nqg + 7) / 8 * 8);
+  uint64_t best = 8;
+  double best_eff = 0.0;
+  for (uint64_t c = 8; c <= std::min<uint64_t>(64, cap); c += 8) {
+    const uint64_t b = nqg * c;
+    const double eff = static_cast<double>(b) / static_cast<double>((b + cus - 1) / cus * cus);
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = c;
+    }
+  }
+  return static_cast<int>(best);
+}
+
+void ensure_tiles(alaya_index *ix, int base_exp, hipStream_t stream) {
+  if (ix->tiles_ready && ix->tiles_exp == base_exp) return;
+  const size_t bytes = alaya_amd::flat_tiles_bytes(ix->stride, ix->n);
+  ix->flat_tiles.reserve(std::max<size_t>(bytes, 256));
+  hip_check(alaya_amd::launch_flat_tiles(ix->base.as<float>(), ix->n, ix->stride, ix->norms.as<float>(),
+                                         ix->has_valid ? ix->valid.as<uint32_t>() : nullptr, base_exp,
+                                         ix->flat_tiles.as<unsigned char>(), stream),
+            "flat tile records");
+  ix->tiles_ready = true;
+  ix->tiles_exp = base_exp;
+}
+
 // Prescan: the same scan over rows 0, S, 2S, ... (S = ALAYA_FLAT_PRESCAN; default 0 = off: on
 // config 2 it cuts fold rounds 846 -> 302 per block but costs more than it saves),
 // then per query the sample's 32nd-best approximate distance as every chunk's starting threshold.
@@ -582,6 +621,41 @@ int flat_chunks(alaya_index *ix, int nqg, uint64_t rows) {
 void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStream_t s) {
   const char *env = std::getenv("ALAYA_FLAT_PRESCAN");
   const uint64_t step = env ? std::strtoull(env, nullptr, 10) : 0;
+  if (p.tiles != nullptr) {
+    // The single-role scan's prescan: group minima over a sample of whole tile records (every S-th;
+    // default S = records / 2048, on when the base has >= 8192 records, ALAYA_FLAT_PRESCAN=S forces S,
+    // 1 turns it off), one block per (query group, group of sampled records); the 32nd smallest
+    // of a query's group minima is its starting threshold (flat_group_threshold_kernel).
+    const uint64_t nt = p.n_scan_tiles;
+    const char *genv = std::getenv("ALAYA_FLAT_PRESCAN_GROUPS");  // diagnostics: groups (default 64)
+    const char *senv = std::getenv("ALAYA_FLAT_PRESCAN_SAMPLE");  // diagnostics: sampled records (2048)
+    const uint64_t want_sample = senv ? std::max<uint64_t>(32, std::strtoull(senv, nullptr, 10)) : 2048;
+    uint64_t S = env ? step : (nt >= 4 * want_sample ? nt / want_sample : 0);
+    if (S < 1 || (env && S < 2)) return;
+    const uint64_t sample = (nt + S - 1) / S;
+    // groups of >= 1 sampled record (32 at the defaults); the minima (groups x nq floats) fit the
+    // candidate buffers (n_chunks >= 8 lists of 32 per query)
+    const uint64_t want_groups = genv ? std::strtoull(genv, nullptr, 10) : 64;
+    const uint64_t groups = std::min<uint64_t>(std::min<uint64_t>(256, want_groups), sample) / 8 * 8;
+    if (groups < static_cast<uint64_t>(alaya_amd::flat_shortlist())) return;
+    alaya_amd::FlatParams q = p;
+    q.tile_step = static_cast<uint32_t>(S);
+    q.n_scan_tiles = sample;
+    q.n_chunks = static_cast<int>(groups);
+    q.tau_init = nullptr;
+    q.out_ids = nullptr;
+    q.out_dists = nullptr;
+    q.flags = nullptr;
+    q.merge_count = nullptr;
+    q.ablate = 0;
+    ix->flat_tau.reserve(p.nq * 4);
+    q.tau_out = ix->flat_tau.as<float>();
+    const int nqg = static_cast<int>((p.nq + alaya_amd::flat_tiles_queries() - 1) / alaya_amd::flat_tiles_queries());
+    hip_check(alaya_amd::launch_flat_scan(q, nqg * q.n_chunks, s), "flat prescan");
+    hip_check(alaya_amd::launch_flat_threshold(q, s), "flat threshold");
+    p.tau_init = q.tau_out;
+    return;
+  }
   if (step < 2 || p.n / step < 1024) return;
   // the slabbed wide scan (rows past 224 floats) reads contiguous rows and has no row_step: its
   // "sample" would be the first n/S rows, so the prescan is off there
@@ -606,7 +680,8 @@ void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStr
 }
 
 alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq, uint32_t k, uint32_t *d_ids,
-                                  float *d_dists, uint32_t *d_flags, int *blocks, hipStream_t stream) {
+                                  float *d_dists, uint32_t *d_flags, int *blocks, hipStream_t stream,
+                                  bool no_single = false) {
   if (!ix->base.ptr) throw ArgError("index has no base vectors");
   if (ix->metric != ALAYA_METRIC_L2) throw ArgError("the flat MFMA path supports the L2 metric");
   if (ix->generic) throw ArgError("the flat MFMA path ranks float32 rows (not the generic non-float order)");
@@ -633,7 +708,7 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
     throw ArgError("ALAYA_FLAT_CONTRACTION must be f16, bf16x3 or f32");
   p.base_exp = alaya_amd::flat_base_exp(ix->max_norm);
   const bool narrow = alaya_amd::flat_query_width(ix->stride) == 0;
-  p.single = (want == "auto" || want == "f16") && narrow && alaya_amd::flat_ws_available(0) &&
+  p.single = !no_single && (want == "auto" || want == "f16") && narrow && alaya_amd::flat_ws_available(0) &&
              std::abs(p.base_exp) <= 60 && ix->max_norm > 0.f && std::isfinite(ix->max_norm);
   p.split = !p.single && want != "f32" && ix->max_norm < 1e18f;
   ix->flat_contraction = p.single ? 2 : (p.split ? 1 : 0);
@@ -649,8 +724,22 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
     p.q_stride = width;
     p.k_acc = width;
   }
-  const int nqg = static_cast<int>((nq + 127) / 128);
-  const int chunks = flat_chunks(ix, nqg, ix->n);
+  // the single pass runs the single-role scan over the cached tile records (ALAYA_FLAT_TILES=0 keeps
+  // the warp-specialised scan, which converts the f32 rows itself)
+  const char *tenv = std::getenv("ALAYA_FLAT_TILES");
+  const bool tiles = p.single && !(tenv && tenv[0] == '0') && alaya_amd::flat_tiles_bytes(ix->stride, ix->n) > 0;
+  int nqg = 0, chunks = 0;
+  if (tiles) {
+    ensure_tiles(ix, p.base_exp, stream);
+    p.tiles = ix->flat_tiles.as<unsigned char>();
+    p.n_scan_tiles = (ix->n + 31) / 32;
+    p.tile_step = 1;
+    nqg = static_cast<int>((nq + alaya_amd::flat_tiles_queries() - 1) / alaya_amd::flat_tiles_queries());
+    chunks = flat_tiles_chunks(ix, nq, p.n_scan_tiles);
+  } else {
+    nqg = static_cast<int>((nq + 127) / 128);
+    chunks = flat_chunks(ix, nqg, ix->n);
+  }
   p.n_chunks = chunks;
   p.row_step = 1;
   const char *spin = std::getenv("ALAYA_FLAT_SPIN_LIMIT");  // debug override (tests force an abort)
@@ -908,6 +997,7 @@ int alaya_index_set_base(alaya_index *ix, const float *rows, uint64_t n, uint32_
     ix->overflow.release();
     ix->overflow_clean = 0;
     ix->norms_ready = false;
+    ix->tiles_ready = false;
     ix->capacity = n;
     ix->upd_graph.reset();
     ix->upd_rows.reset();
@@ -1016,6 +1106,7 @@ void write_rows_locked(alaya_index *ix, uint64_t first, const float *rows, uint6
   hip_check(hipStreamSynchronize(ix->stream), "sync");
   ix->n = std::max(ix->n, first + count);
   ix->norms_ready = false;
+  ix->tiles_ready = false;
 }
 
 void write_edges_locked(alaya_index *ix, const uint32_t *ids, const uint32_t *edges, uint64_t count) {
@@ -1046,6 +1137,7 @@ void set_valid_locked(alaya_index *ix, uint64_t id, bool valid) {
   hip_check(hipMemcpy(&w, dw, 4, hipMemcpyDeviceToHost), "read bitmap");
   w = valid ? (w | (1u << (id & 31))) : (w & ~(1u << (id & 31)));
   hip_check(hipMemcpy(dw, &w, 4, hipMemcpyHostToDevice), "write bitmap");
+  ix->tiles_ready = false;  // the records carry +inf norms for cleared rows
 }
 
 }  // namespace
@@ -1795,9 +1887,9 @@ int alaya_index_flat_search(alaya_index *ix, const float *queries, uint64_t nq, 
       uint64_t nflag = 0;
       for (uint64_t q = 0; q < nq; ++q) nflag += flags[q] ? 1 : 0;
       if (nflag * 100 > nq) {
-        p.single = 0;
-        p.split = ix->max_norm < 1e18f;
-        ix->flat_contraction = p.split ? 1 : 0;
+        p = flat_params(ix, ix->q_buf.as<float>(), nq, k, ix->id_buf.as<uint32_t>(), ix->dist_buf.as<float>(),
+                        ix->flag_buf.as<uint32_t>(), &blocks, ix->stream, /*no_single=*/true);
+        flat_prescan(ix, p, &blocks, ix->stream);
         run();
       }
     }

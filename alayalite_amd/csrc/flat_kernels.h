@@ -39,6 +39,10 @@ struct FlatParams {
   uint32_t *merge_count;  // diagnostics only (nullable): merges per block
   uint32_t spin_limit; // warp-specialised scan: LDS-flag polls before a block aborts (its queries are
                        // then flagged for the exhaustive redo); 1 << 20 unless ALAYA_FLAT_SPIN_LIMIT
+  const unsigned char *tiles;  // single-role f16 scan (non-null selects it): the base's tile records
+                               // (launch_flat_tiles), rows already scaled by 2^base_exp
+  uint64_t n_scan_tiles;       // records the scan visits: 0, tile_step, 2 tile_step, ... (split over the chunks)
+  uint32_t tile_step;          // 1 = every record; the prescan's sample takes every tile_step-th
 };
 
 int flat_shortlist();
@@ -56,6 +60,13 @@ hipError_t launch_pad_queries(const float *src, uint64_t nq, uint32_t dim, uint3
                               hipStream_t s);
 hipError_t launch_row_norms(const float *base, uint64_t n, uint32_t stride, float *norms, hipStream_t s);
 hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s);
+// Tile records of the single-role f16 scan for rows of `stride` floats: bytes for n rows (0: that
+// scan does not cover this stride); built from the f32 rows, their |b|^2 and the validity bitmap
+size_t flat_tiles_bytes(uint32_t stride, uint64_t n);
+hipError_t launch_flat_tiles(const float *base, uint64_t n, uint32_t stride, const float *norms, const uint32_t *valid,
+                             int base_exp, unsigned char *out, hipStream_t s);
+// queries per block of the single-role f16 scan
+int flat_tiles_queries();
 hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s);
 hipError_t launch_flat_threshold(const FlatParams &p, hipStream_t s);
 

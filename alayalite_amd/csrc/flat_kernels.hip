@@ -198,7 +198,9 @@ __device__ __forceinline__ void init_shortlists(const FlatParams &p, uint64_t q0
     S.ld[r] = FLT_MAX;
     S.li[r] = 0xffffffffu;
     const uint64_t qi = q0 + reg_query(R0 + r, h);
-    S.tau[r] = (p.tau_init && qi < p.nq) ? p.tau_init[qi] : FLT_MAX;
+    // a slot past the last query takes no candidates (-FLT_MAX: no `d < tau` holds), so a partial
+    // query group does no append or fold work for its empty slots
+    S.tau[r] = qi < p.nq ? (p.tau_init ? p.tau_init[qi] : FLT_MAX) : -FLT_MAX;
     S.cnt[r] = 0;
   }
 }
@@ -219,10 +221,16 @@ __device__ __forceinline__ void store_shortlists(const FlatParams &p, uint64_t q
   }
 }
 
+template <int kB, int NR, int R0>
+__device__ __forceinline__ void fold_rounds(const FlatParams &p, uint32_t need, bool last, ShortlistsT<NR> &S,
+                                            float *bd, uint32_t *bi);
+
 // Candidate handling of one 32-row tile: approximate distances a = |b|^2 - 2 c[r] below the
 // query's threshold are appended to its LDS buffer (bd/bi, a stack per query), then the fold
-// rounds that became due run.  last: the wave's final tile (every buffer is drained).
-template <int kB = kBuf, int NR = 16, int R0 = 0>
+// rounds that became due run.  last: the wave's final tile (every buffer is drained).  kDv: c
+// already holds the approximate distances (the single-role f16 scan computes them first to test
+// the whole tile at once); bn is then unused.
+template <int kB = kBuf, int NR = 16, int R0 = 0, bool kDv = false>
 __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32xN<NR> &c, float bn, uint32_t rid,
                                                 uint64_t live_mask, bool last, ShortlistsT<NR> &S, float *bd,
                                                 uint32_t *bi, uint64_t &t_app, uint64_t &t_fold) {
@@ -237,7 +245,7 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32xN
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int qloc = reg_query(R0 + r, h);  // wave-local query of register r, half h
-    const float dv = fmaf(-2.0f, c[r], bn);
+    const float dv = kDv ? c[r] : fmaf(-2.0f, c[r], bn);
     // the compare's lane mask straight from v_cmp (llvm.amdgcn.fcmp, predicate OLT = 4), no
     // bool round trip through a VGPR
     const uint64_t mk = __builtin_amdgcn_fcmpf(dv, S.tau[r], 4) & live_mask;
@@ -272,11 +280,21 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32xN
     S.nonempty &= ~need;
     need = 0;
   }
-  // Fold rounds for the registers in `need`.  One copy of the
-  // fold body (a uniform loop over `need`, the register picked by value): unrolling it per
-  // register would put ~48 KB of code in the loop and thrash the instruction cache.
   const uint64_t tf = p.merge_count ? __builtin_amdgcn_s_memtime() : 0;
   t_app += tf - ta;
+  fold_rounds<kB, NR, R0>(p, need, last, S, bd, bi);
+  t_fold += (p.merge_count ? __builtin_amdgcn_s_memtime() : 0) - tf;
+}
+
+// Fold rounds for the registers in `need` (each: the newest 32 buffered entries of its two queries,
+// one per half; last: repeated until the buffer is empty).  One copy of the fold body (a uniform
+// loop over `need`, the register picked by value): unrolling it per register would put ~48 KB of
+// code in the loop and thrash the instruction cache.
+template <int kB, int NR, int R0>
+__device__ __forceinline__ void fold_rounds(const FlatParams &p, uint32_t need, bool last, ShortlistsT<NR> &S,
+                                            float *bd, uint32_t *bi) {
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
   if (need) {
     wave_fence();
     do {
@@ -322,7 +340,6 @@ __device__ __forceinline__ void tile_candidates(const FlatParams &p, const f32xN
     } while (need);
     wave_fence();
   }
-  t_fold += (p.merge_count ? __builtin_amdgcn_s_memtime() : 0) - tf;
 }
 
 template <int K, bool kSplit>
@@ -818,6 +835,313 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
                                           qexp);
     }
   }
+}
+
+// --------------------------------------------------------------------------------------------
+// Single-role single-pass scan over prebuilt f16 tile records (round 6, the default for narrow rows
+// in the single-pass contraction).  The warp-specialised scan above converts every f32 row tile
+// to f16 in each of the 8 blocks that scan it and hands each 32x32 contraction from a producer to
+// a consumer through LDS flags; the tile records below are converted once per base (cached on the
+// index) and laid out as the MFMA's B fragments in lane order, so a block stages a tile with one
+// lane-linear global->LDS DMA per 1 KB piece and every wave reads its fragments with conflict-free
+// ds_read_b128.  512 threads = 8 waves (two per SIMD), each holding 32 queries as A fragments,
+// 256 queries per block sharing every staged tile; each wave contracts the tile (K/16 MFMAs),
+// forms the 1,024 approximate distances and tests them against its queries' thresholds in one
+// pass, and only a tile with a candidate (or a due fold) enters tile_candidates -- the same
+// appends, fold rounds and register shortlists as the other scans, so the merge and its error
+// bound (the single pass's) are unchanged.  One raw s_barrier per tile orders the ring: after it,
+// every wave's pieces of tile j have landed (each wave waited for its own DMA) and every wave has
+// finished tile j - 1, whose slot is then refilled with tile j + kD - 1.
+// --------------------------------------------------------------------------------------------
+// Tile record T (rows 32T .. 32T+31): K/16 pieces of 64 lanes x 8 f16 -- lane l: row 32T + (l & 31),
+// k = (l >> 5) K/2 + 8 st + j, the k map of the other scans' A fragments -- each element
+// f16(x 2^base_exp) exactly as the warp-specialised scan stages it; then a 256-byte tail: the 32
+// rows' |b|^2 (+inf for a row past n or cleared in the validity bitmap: its approximate distance
+// is +inf and fails every `d < tau`, so the scan reads no bitmap) and 32 zero words.
+template <int K>
+constexpr int tiles_rec() { return K / 16 * 1024 + 256; }
+
+template <int K>
+__global__ void flat_tiles_kernel(const float *base, uint64_t n, uint32_t stride, const float *norms,
+                                  const uint32_t *valid, int base_exp, uint64_t n_tiles, unsigned char *out) {
+  constexpr int kSteps = K / 16;
+  constexpr int kPer = kSteps * 64 + 64;  // threads per record: one per 16-byte piece lane, 64 for the tail
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t T = g / kPer;
+  if (T >= n_tiles) return;
+  const int w = static_cast<int>(g % kPer);
+  unsigned char *rec = out + T * tiles_rec<K>();
+  if (w < kSteps * 64) {
+    const int st = w >> 6, l = w & 63;
+    const uint64_t row = T * 32 + (l & 31);
+    const uint32_t e0 = (l >> 5) * (K / 2) + 8 * st;
+    f16x8 v;
+    if (row < n) {
+      const float4 a = *reinterpret_cast<const float4 *>(base + row * stride + e0);
+      const float4 b = *reinterpret_cast<const float4 *>(base + row * stride + e0 + 4);
+      v[0] = static_cast<_Float16>(ldexpf(a.x, base_exp));
+      v[1] = static_cast<_Float16>(ldexpf(a.y, base_exp));
+      v[2] = static_cast<_Float16>(ldexpf(a.z, base_exp));
+      v[3] = static_cast<_Float16>(ldexpf(a.w, base_exp));
+      v[4] = static_cast<_Float16>(ldexpf(b.x, base_exp));
+      v[5] = static_cast<_Float16>(ldexpf(b.y, base_exp));
+      v[6] = static_cast<_Float16>(ldexpf(b.z, base_exp));
+      v[7] = static_cast<_Float16>(ldexpf(b.w, base_exp));
+    } else {
+      for (int j = 0; j < 8; ++j) v[j] = static_cast<_Float16>(0.f);
+    }
+    *reinterpret_cast<f16x8 *>(rec + st * 1024 + l * 16) = v;
+  } else {
+    const int l = w - kSteps * 64;
+    float x = 0.f;
+    if (l < 32) {
+      const uint64_t row = T * 32 + l;
+      const bool live = row < n && (valid == nullptr || ((valid[row >> 5] >> (row & 31)) & 1u));
+      x = live ? norms[row] : __builtin_inff();
+    }
+    reinterpret_cast<float *>(rec + kSteps * 1024)[l] = x;
+  }
+}
+
+// candidate buffer entries per query: a whole tile of appends above the 32 a due fold may leave
+// (the `need` rule: a buffer holding more than kB - 32 entries is folded before the next tile)
+template <int K>
+constexpr int tiles_buf() { return 64; }
+// tile slots: j (being read) and up to kD - 1 records in flight, as many as the 160 KB leave beside
+// the candidate buffers, at most ALAYA_FLAT_TILES_RING (diagnostics builds; measured: 3 slots as
+// fast as more -- the ring is not what bounds a step)
+#ifndef ALAYA_FLAT_TILES_RING
+#define ALAYA_FLAT_TILES_RING 3
+#endif
+template <int K>
+constexpr int tiles_ring() {
+  constexpr int fit = static_cast<int>((160 * 1024 - 8 * 32 * tiles_buf<K>() * 8) / (K / 16 * 1024 + 256));
+  return fit < ALAYA_FLAT_TILES_RING ? fit : ALAYA_FLAT_TILES_RING;
+}
+template <int K>
+constexpr size_t tiles_lds() {
+  return static_cast<size_t>(tiles_ring<K>()) * tiles_rec<K>() + static_cast<size_t>(8) * 32 * tiles_buf<K>() * 8;
+}
+template <int K>
+constexpr bool tiles_fits() {
+  return tiles_lds<K>() <= 160 * 1024 && tiles_buf<K>() >= 2 * kTile && tiles_ring<K>() >= 2;
+}
+
+static_assert(tiles_fits<32>() && tiles_fits<64>() && tiles_fits<96>() && tiles_fits<128>() && tiles_fits<160>() &&
+                  tiles_fits<192>() && tiles_fits<224>(),
+              "single-role f16 scan: tile ring / candidate buffers");
+
+// this wave's DMA pieces of one record: pieces w, w + 8, ... of K/16 fragment pieces (16 B per lane)
+// and the tail (4 B per lane)
+template <int K>
+__device__ __forceinline__ void tiles_issue(const unsigned char *src, unsigned char *slot, int wave, int lane) {
+  constexpr int kSteps = K / 16;
+#pragma unroll
+  for (int pc = 0; pc < kSteps + 1; pc += 8) {
+    const int piece = pc + wave;
+    if (piece < kSteps) {
+      __builtin_amdgcn_global_load_lds(static_cast<const void *>(src + piece * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void *)(slot + piece * 1024), 16, 0, 0);
+    } else if (piece == kSteps) {
+      __builtin_amdgcn_global_load_lds(static_cast<const void *>(src + kSteps * 1024 + lane * 4),
+                                       (__attribute__((address_space(3))) void *)(slot + kSteps * 1024), 4, 0, 0);
+    }
+  }
+}
+
+// kMin: the prescan's form -- no shortlists: each block is one group of sampled records, and each
+// query's smallest approximate distance over the group is written to cand_d[group * nq + query]
+// (flat_group_threshold_kernel then takes the 32nd smallest of the groups' minima per query).
+template <int K, bool kMin>
+__global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
+  static_assert(K % 16 == 0 && K <= 224, "narrow rows");
+  constexpr int kSteps = K / 16;
+  constexpr int kRec = tiles_rec<K>();
+  constexpr int kB = tiles_buf<K>();
+  constexpr int kD = tiles_ring<K>();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar branches on it
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  float *bd = reinterpret_cast<float *>(smem + kD * kRec) + wave * 32 * kB * 2;  // 32 queries x kB
+  uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
+
+  // XCD-aware: the query groups of a chunk are consecutive multiples of 8 apart (one XCD)
+  const int nqg = static_cast<int>((p.nq + 255) / 256);
+  const int b = blockIdx.x;
+  const int qg = (b / 8) % nqg;
+  const int chunk = (b % 8) + 8 * (b / (8 * nqg));
+  if (chunk >= p.n_chunks) return;  // the whole block
+  const uint64_t per = (p.n_scan_tiles + p.n_chunks - 1) / p.n_chunks;
+  const uint64_t j0 = chunk * per;
+  const uint64_t j1 = min(p.n_scan_tiles, j0 + per);
+  const int ntiles = j1 > j0 ? static_cast<int>(j1 - j0) : 0;
+  const uint64_t q0 = static_cast<uint64_t>(qg) * 256 + wave * 32;
+
+  // A fragments of the wave's 32 queries, each scaled by its own 2^t (the ws scan's producer code).
+  // The loads are unconditional (a clamped row and column, the value selected afterwards): a load
+  // under a per-element condition makes the compiler wait for each one in turn, which a prescan
+  // block of 16 records cannot amortise.
+  f16x8 aq[kSteps];
+  int t_own = 0;
+  {
+    const uint64_t qi = q0 + col;
+    const bool qok = qi < p.nq;
+    const uint32_t e0 = h * (K / 2);
+    const float *qp = p.queries + (qok ? qi : 0) * p.q_stride;
+    float x[kSteps * 8];
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t e = e0 + 8 * s + j;
+        const float v = qp[e < p.dim ? e : p.dim - 1];
+        x[8 * s + j] = (qok && e < p.dim) ? v : 0.f;
+      }
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSteps * 8; ++i) mx = fmaxf(mx, fabsf(x[i]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    t_own = f16_exp(mx);
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) aq[s][j] = static_cast<_Float16>(ldexpf(x[8 * s + j], t_own));
+  }
+  // -2 x the scale-back 2^-(s + t) of register r's query: a = fma(m2u, C~, |b|^2)
+  f32xN<16> m2u;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) m2u[r] = ldexpf(-2.0f, -(p.base_exp + __shfl(t_own, reg_query(r, h))));
+  ShortlistsT<16> S;
+  init_shortlists<16, 0>(p, q0, h, S);
+  f32xN<16> rmin;  // kMin: running minimum of register r's query over the group
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rmin[r] = __builtin_inff();
+
+  const unsigned char *recs = p.tiles;
+  auto rec_of = [&](int jj) { return recs + (j0 + jj) * p.tile_step * kRec; };
+  // pieces this wave issues per record (wave-uniform): the vmcnt count of one record
+  const int pw = wave < kSteps + 1 ? (kSteps + 1 - wave + 7) / 8 : 0;
+#pragma unroll
+  for (int jj = 0; jj < kD - 1; ++jj)
+    if (jj < ntiles) tiles_issue<K>(rec_of(jj), smem + jj * kRec, wave, lane);
+  // diagnostics (p.merge_count): per-wave s_memtime totals of the wait + barrier, the contraction
+  // and threshold test, and the candidate handling; p.ablate 1 skips the candidate handling, 3 the
+  // contraction too (the DMA ring and the barriers alone)
+  const bool diag = p.merge_count != nullptr;
+  uint64_t t_wait = 0, t_mm = 0, t_cand = 0, sink = 0;
+  const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
+  for (int jj = 0; jj < ntiles; ++jj) {
+    const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
+    // this wave's pieces of tile jj have landed: at most the pieces of tiles jj + 1 .. jj + kD - 2
+    // stay in flight (and its LDS reads of tile jj - 1 are done before the barrier lets that slot
+    // be refilled)
+    asm volatile("" ::: "memory");
+    if (jj + kD - 2 < ntiles) {
+      if (pw == 2) __builtin_amdgcn_s_waitcnt(0x70 | (2 * (kD - 2)));
+      else __builtin_amdgcn_s_waitcnt(0x70 | (kD - 2));
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x70);
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const uint64_t tm = diag ? __builtin_amdgcn_s_memtime() : 0;
+    if (diag) t_wait += tm - tw;
+    const int slot = jj % kD;
+    if (jj + kD - 1 < ntiles) tiles_issue<K>(rec_of(jj + kD - 1), smem + ((jj + kD - 1) % kD) * kRec, wave, lane);
+    const unsigned char *tl = smem + slot * kRec;
+    if (p.ablate == 3) continue;
+    // every B fragment of the tile in flight at once (one LDS latency, not one per MFMA pair)
+    f16x8 bf[kSteps];
+#pragma unroll
+    for (int st = 0; st < kSteps; ++st) bf[st] = *reinterpret_cast<const f16x8 *>(tl + st * 1024 + lane * 16);
+    const float bn = reinterpret_cast<const float *>(tl + kSteps * 1024)[col];
+    // all reads issued before the first MFMA waits on one (K <= 128; wider rows would spill)
+    if constexpr (kSteps <= 8) __builtin_amdgcn_sched_barrier(0);
+    f32x16 c = {};
+#pragma unroll
+    for (int st = 0; st < kSteps; ++st) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[st], bf[st], c, 0, 0, 0);
+    if constexpr (kMin) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) rmin[r] = fminf(rmin[r], fmaf(m2u[r], c[r], bn));
+      continue;
+    }
+    const uint64_t rid = ((j0 + jj) * p.tile_step) * 32 + col;
+    f32xN<16> dv;
+    uint64_t any = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dv[r] = fmaf(m2u[r], c[r], bn);
+      any |= __builtin_amdgcn_fcmpf(dv[r], S.tau[r], 4);
+    }
+    const bool last = jj == ntiles - 1;
+    const uint64_t tc = diag ? __builtin_amdgcn_s_memtime() : 0;
+    if (diag) t_mm += tc - tm;
+    if (p.ablate == 1) {
+      sink += any;
+      continue;
+    }
+    // Candidates are rare once the prescan threshold is in (~10 per query and chunk), so the tile
+    // test above keeps only their union; a tile that has one recomputes each register's lane mask
+    // (the asm keeps the compiler from holding 16 masks in SGPRs across the common path), appends,
+    // and folds a buffer that could overflow on the next tile (more than kB - 32 entries).  The
+    // last tile drains every buffer.
+    uint32_t need = 0;
+    if (any) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float d = dv[r];
+        asm volatile("" : "+v"(d));
+        const uint64_t m = __builtin_amdgcn_fcmpf(d, S.tau[r], 4);
+        if (!m) continue;
+        const uint32_t lo = static_cast<uint32_t>(m), hi = static_cast<uint32_t>(m >> 32);
+        const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u))) -
+                          (h ? __popc(lo) : 0);
+        const int cr = S.cnt[r];
+        if ((m >> lane) & 1ull) {
+          const int at = reg_query(r, h) * kB + cr + below;
+          bd[at] = d;
+          bi[at] = static_cast<uint32_t>(rid);
+        }
+        const int nc = cr + (h ? __popc(hi) : __popc(lo));
+        S.cnt[r] = nc;
+        S.nonempty |= 1u << r;
+        if (__builtin_amdgcn_ballot_w64(nc > kB - kTile)) need |= 1u << r;
+      }
+    }
+    if (last) need |= S.nonempty;
+    if (p.ablate == 4) {  // diagnostics: appends only, buffers dropped instead of folded
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (need & (1u << r)) S.cnt[r] = 0;
+      need = 0;
+    }
+    if (need) fold_rounds<kB, 16, 0>(p, need, last, S, bd, bi);
+    if (diag) t_cand += __builtin_amdgcn_s_memtime() - tc;
+  }
+  if constexpr (kMin) {
+    // the group's minimum of each query: over the 32 rows (lanes) of its half
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = rmin[r];
+      v = fminf(v, swz_f<1>(v));
+      v = fminf(v, swz_f<2>(v));
+      v = fminf(v, swz_f<4>(v));
+      v = fminf(v, swz_f<8>(v));
+      v = fminf(v, swz_f<16>(v));
+      const uint64_t qi = q0 + reg_query(r, h);
+      if (col == 0 && qi < p.nq) p.cand_d[static_cast<uint64_t>(chunk) * p.nq + qi] = v;
+    }
+    return;
+  }
+  if (diag && lane == 0) {  // diagnostics rows (tools/ab_flat.py --diag): total, wait, contraction, candidates
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * 8 + wave) * 4;
+    st[0] = __builtin_amdgcn_s_memtime() - t_start;
+    st[1] = t_wait;
+    st[2] = t_mm;
+    st[3] = t_cand + (sink == 0xffffffffffffffffull ? 1 : 0);
+  }
+  store_shortlists<16, 0>(p, q0, chunk, S);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1367,6 +1691,33 @@ __global__ void __launch_bounds__(64) flat_threshold_kernel(FlatParams p) {
   }
 }
 
+// Prescan threshold of the single-role scan: one wave per query takes the 32nd smallest of the
+// n_chunks group minima (each a distinct row's approximate distance) as T and writes
+// nextafter(T, +inf): at least 32 rows then pass the full scan's strict `d < tau` and reach the
+// merged shortlist, which is all flat_merge_kernel's bound needs (cutoff = min(list 32nd, T)).
+// Fewer than 32 groups, or minima that are not finite: FLT_MAX (no threshold).
+__global__ void __launch_bounds__(64) flat_group_threshold_kernel(FlatParams p) {
+  const int lane = lane_id();
+  const int G = p.n_chunks;
+  for (uint64_t qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
+    // rank of each minimum by (value, group): the entry of rank kL - 1 is the 32nd smallest
+    float th = FLT_MAX;
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int g = g0 + lane;
+      const float v = g < G ? p.cand_d[static_cast<uint64_t>(g) * p.nq + qi] : FLT_MAX;
+      int rank = 0;
+      for (int o = 0; o < G; ++o) {
+        const float w = p.cand_d[static_cast<uint64_t>(o) * p.nq + qi];
+        rank += (w < v || (w == v && o < g)) ? 1 : 0;
+      }
+      const uint64_t m = __ballot(g < G && rank == kL - 1);
+      if (m) th = __shfl(v, __ffsll(static_cast<unsigned long long>(m)) - 1);
+    }
+    if (lane == 0)
+      p.tau_out[qi] = (G < kL || !(th < FLT_MAX)) ? FLT_MAX : nextafterf(th, FLT_MAX);
+  }
+}
+
 __global__ void row_norms_kernel(const float *base, uint64_t n, uint32_t stride, float *norms) {
   const uint64_t row = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1483,7 +1834,52 @@ hipError_t launch_pad_queries(const float *src, uint64_t nq, uint32_t dim, uint3
   return hipGetLastError();
 }
 
+size_t flat_tiles_bytes(uint32_t stride, uint64_t n) {
+  if (stride == 0 || stride > 224 || stride % 32 != 0) return 0;
+  return static_cast<size_t>((n + 31) / 32) * (stride / 16 * 1024 + 256);
+}
+
+int flat_tiles_queries() { return 256; }
+
+hipError_t launch_flat_tiles(const float *base, uint64_t n, uint32_t stride, const float *norms, const uint32_t *valid,
+                             int base_exp, unsigned char *out, hipStream_t s) {
+  const uint64_t n_tiles = (n + 31) / 32;
+  if (n_tiles == 0) return hipSuccess;
+  const uint64_t threads = n_tiles * (stride / 16 * 64 + 64);
+  const dim3 grid(static_cast<unsigned>((threads + 255) / 256));
+  switch (stride) {
+#define ALAYA_TILES(K)                                                                                        \
+  case K:                                                                                                     \
+    hipLaunchKernelGGL(flat_tiles_kernel<K>, grid, dim3(256), 0, s, base, n, stride, norms, valid, base_exp, \
+                       n_tiles, out);                                                                         \
+    break;
+    ALAYA_TILES(32) ALAYA_TILES(64) ALAYA_TILES(96) ALAYA_TILES(128) ALAYA_TILES(160) ALAYA_TILES(192)
+    ALAYA_TILES(224)
+#undef ALAYA_TILES
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
+  if (p.tiles != nullptr) {
+    // p.tau_out set: the prescan's group minima (ring only in LDS, no candidate buffers)
+    switch (p.stride) {
+#define ALAYA_TILES(K)                                                                                          \
+  case K:                                                                                                       \
+    if (p.tau_out)                                                                                             \
+      hipLaunchKernelGGL((flat_scan_tiles_kernel<K, true>), dim3(blocks), dim3(512),                           \
+                         static_cast<size_t>(tiles_ring<K>()) * tiles_rec<K>(), s, p);                        \
+    else                                                                                                        \
+      hipLaunchKernelGGL((flat_scan_tiles_kernel<K, false>), dim3(blocks), dim3(512), tiles_lds<K>(), s, p);   \
+    break;
+      ALAYA_TILES(32) ALAYA_TILES(64) ALAYA_TILES(96) ALAYA_TILES(128) ALAYA_TILES(160) ALAYA_TILES(192)
+      ALAYA_TILES(224)
+#undef ALAYA_TILES
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   const size_t lds = flat_scan_lds(p.stride);
   if (lds == 0) return hipErrorInvalidValue;
   constexpr int TT = kWideTiles;
@@ -1536,7 +1932,10 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
 
 hipError_t launch_flat_threshold(const FlatParams &p, hipStream_t s) {
   const int grid = static_cast<int>(p.nq < 4096 ? p.nq : 4096);
-  hipLaunchKernelGGL(flat_threshold_kernel, dim3(grid), dim3(64), 0, s, p);
+  if (p.tiles != nullptr)
+    hipLaunchKernelGGL(flat_group_threshold_kernel, dim3(grid), dim3(64), 0, s, p);
+  else
+    hipLaunchKernelGGL(flat_threshold_kernel, dim3(grid), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 

@@ -195,6 +195,7 @@ class ShardPipeline:
         self.packed = [None, None]  # packed keys of the batch in each slot (compute stream)
         self.gpu = self.device.type == "cuda"
         self._masked = None
+        self.closed = False
         if self.gpu:
             if reserve_cus > 0:
                 from ._native import _ext
@@ -248,6 +249,8 @@ class ShardPipeline:
     def run(self, batches):
         """Search + exchange every batch (device query tensors); returns the merged (ids, dists) per
         batch, produced on the exchange stream (synchronise before reading them on the host)."""
+        if self.closed:
+            raise RuntimeError("ShardPipeline used after close()")
         out = [None] * len(batches)
         if not batches:
             return out
@@ -280,6 +283,8 @@ class ShardPipeline:
             torch.cuda.synchronize(self.device)
             _ext.stream_destroy(self._masked)
             self._masked = None
+            self.compute = None  # the ExternalStream wrapped the freed handle
+        self.closed = True
 
     def __enter__(self):
         return self

@@ -358,15 +358,18 @@ def recall(ids, gt):
     return hits / float(ids.size)
 
 
-def flat_scan_kernel_name(dim):
+def flat_scan_kernel_name(dim, contraction=None):
     """The scan kernel launch_flat_scan (csrc/flat_kernels.hip) dispatches for rows of `dim` floats:
-    the slabbed wide scan past 224 columns, else the warp-specialised split scan unless the f32
-    contraction or the single-role scan is forced by environment."""
+    the slabbed wide scan past 224 columns; for the single-pass f16 contraction the single-role scan
+    over the cached tile records unless ALAYA_FLAT_TILES=0; else the warp-specialised scan unless the
+    f32 contraction or the diagnostics' single-role f32 scan is forced by environment."""
     if (dim + 31) // 32 * 32 > 224:
         return "flat_scan_wide_kernel"
     if (os.environ.get("ALAYA_FLAT_F32") or os.environ.get("ALAYA_FLAT_WS0")
             or os.environ.get("ALAYA_FLAT_CONTRACTION") == "f32"):
         return "flat_scan_kernel"
+    if contraction == "f16" and os.environ.get("ALAYA_FLAT_TILES", "1") != "0":
+        return "flat_scan_tiles_kernel"
     return "flat_scan_ws_kernel"
 
 
@@ -423,12 +426,12 @@ def run_flat(args):
         ok += int(set(r.tolist()) == set(got[qi].tolist()))
     flops = 2.0 * n * nq * dim
     tf = flops / (ms * 1e-3) / 1e12
-    scan = flat_scan_kernel_name(dim)
     # the roofline is the issued contraction's own MFMA peak (alaya_index_flat_last_contraction):
     # the single-pass f16 (default for rows of <= 224 floats) issues one f16 product per f32 product,
     # so its ceiling is the dense f16 peak (16 x 157.3 TF); the bf16 hi/lo split issues 3 bf16
     # products per f32 product (dense bf16 peak / 3); the f32 contraction runs at the 157.3 TF f32 peak
     contraction = {0: "f32", 1: "bf16x3", 2: "f16"}[index.flat_contraction()]
+    scan = flat_scan_kernel_name(dim, contraction)
     mfma_peak = {"f32": 157.3, "bf16x3": round(16 * 157.3 / 3, 1), "f16": round(16 * 157.3, 1)}[contraction]
     # HBM traffic of the scan from the committed PMC passes on this workload and kernel
     # (tools/run_pmc_flat.sh; latest round first)

@@ -8,18 +8,23 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["f16", "split", "f32", "f16-prescan2", "f32-prescan3", "f16-ws1", "split-ws1"],
+@pytest.fixture(params=["f16", "split", "f32", "f16-prescan2", "f32-prescan3", "f16-ws", "f16-ws1", "split-ws1"],
                 autouse=True)
 def flat_mode(request, monkeypatch):
     """Every shortlist contraction: the single-pass f16 on power-of-two-scaled operands (the default
     for rows of <= 224 floats), the bf16 hi/lo split (ALAYA_FLAT_CONTRACTION=bf16x3; the default for
     wider rows) and the f32 MFMA (ALAYA_FLAT_CONTRACTION=f32).  The exact rescoring and the bound
-    check make the answer identical.  The prescan (a scan over every S-th row that seeds each chunk's
-    threshold; off by default, ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes.  The
-    warp-specialised scan runs two consumer waves per producer by default; -ws1 forces one
-    (ALAYA_FLAT_WS2=0)."""
-    for var in ("ALAYA_FLAT_F32", "ALAYA_FLAT_PRESCAN", "ALAYA_FLAT_WS2", "ALAYA_FLAT_CONTRACTION"):
+    check make the answer identical.  The single pass runs the single-role scan over the index's
+    cached f16 tile records by default; -ws modes force the warp-specialised scan
+    (ALAYA_FLAT_TILES=0), which converts the f32 rows itself.  The prescan (a scan over every S-th
+    row -- every S-th tile record in the single-role scan -- that seeds each chunk's threshold;
+    ALAYA_FLAT_PRESCAN=S) is forced on by the -prescanS modes.  The warp-specialised scan runs two
+    consumer waves per producer by default; -ws1 forces one (ALAYA_FLAT_WS2=0)."""
+    for var in ("ALAYA_FLAT_F32", "ALAYA_FLAT_PRESCAN", "ALAYA_FLAT_WS2", "ALAYA_FLAT_CONTRACTION",
+                "ALAYA_FLAT_TILES"):
         monkeypatch.delenv(var, raising=False)
+    if "-ws" in request.param:
+        monkeypatch.setenv("ALAYA_FLAT_TILES", "0")
     if request.param.endswith("-ws1"):
         monkeypatch.setenv("ALAYA_FLAT_WS2", "0")
     if request.param.startswith("f32"):
@@ -169,7 +174,7 @@ def test_flat_spin_abort_is_flagged_and_redone(native, orc, flat_mode, monkeypat
     exhaustive redo still returns the exact answer."""
     import torch
 
-    if flat_mode not in ("f16", "f16-ws1", "split", "split-ws1"):
+    if flat_mode not in ("f16-ws", "f16-ws1", "split", "split-ws1"):
         pytest.skip("the ring protocol belongs to the warp-specialised scan (f16 and split contractions)")
     group = 32 if flat_mode.endswith("-ws1") else 16  # queries per consumer wave
     monkeypatch.setenv("ALAYA_FLAT_SPIN_LIMIT", "0")
@@ -249,3 +254,78 @@ def test_calc_gt_device_matches_calc_gt(native):
     ids, dists = alayalite_amd.utils.calc_gt_device(base, q, 10)
     assert ids.dtype == np.int32 and dists.shape == (25, 10)
     assert np.array_equal(ids, calc_gt(base, q, 10))
+
+
+def _clib():
+    import ctypes
+    import os
+
+    import alayalite_amd  # noqa: F401  (builds nothing: the in-tree library must exist)
+
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(alayalite_amd.__file__), "libalaya_hip.so"))
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    lib.alaya_index_create.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.alaya_index_destroy.argtypes = [vp]
+    lib.alaya_index_set_base.argtypes = [vp, vp, u64, u32, i32, vp]
+    lib.alaya_index_flat_search.argtypes = [vp, vp, u64, u32, vp, vp, vp]
+    lib.alaya_index_reserve.argtypes = [vp, u64]
+    lib.alaya_index_write_rows.argtypes = [vp, u64, vp, u64]
+    lib.alaya_index_set_valid.argtypes = [vp, u64, i32]
+    lib.alaya_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def test_flat_tile_records_follow_updates(orc, flat_mode):
+    """The single-role scan's tile records are cached on the index (f16 rows, norms, +inf for
+    cleared rows): a removal (alaya_index_set_valid), a re-validation and rows written past the old
+    end (alaya_index_reserve + write_rows, a partial last tile) must all reach the next flat search,
+    whose answer equals the oracle's over the valid rows, in every mode."""
+    import ctypes
+
+    lib = _clib()
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rng = np.random.default_rng(808)
+    n, d, k = 3000, 64, 10
+    base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
+    extra = np.ascontiguousarray(rng.random((45, d), dtype=np.float32))
+    q = np.ascontiguousarray(rng.random((40, d), dtype=np.float32))
+    ix = ctypes.c_void_p()
+    assert lib.alaya_index_create(0, ctypes.byref(ix)) == 0
+    try:
+        assert lib.alaya_index_set_base(ix, ptr(base), n, d, 0, None) == 0, lib.alaya_last_error()
+
+        def flat(rows, valid):
+            ids = np.zeros((len(q), k), np.uint32)
+            dists = np.zeros((len(q), k), np.float32)
+            redo = ctypes.c_uint32()
+            assert lib.alaya_index_flat_search(ix, ptr(q), len(q), k, ptr(ids), ptr(dists),
+                                               ctypes.byref(redo)) == 0, lib.alaya_last_error()
+            live = np.nonzero(valid)[0]
+            ref_i, ref_d = _exact(orc, rows[live], q, k)
+            assert np.array_equal(ids, live[ref_i].astype(np.uint32))
+            assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
+
+        valid = np.ones(n, bool)
+        flat(base, valid)
+        # capacity for the appended rows; this also materialises the validity bitmap
+        assert lib.alaya_index_reserve(ix, n + len(extra)) == 0, lib.alaya_last_error()
+        flat(base, valid)
+        # remove every query's current nearest row, then put one back
+        for a in range(len(q)):
+            near = int(np.argmin(((base - q[a]) ** 2).sum(1)))
+            assert lib.alaya_index_set_valid(ix, near, 0) == 0, lib.alaya_last_error()
+            valid[near] = False
+        flat(base, valid)
+        back = int(np.nonzero(~valid)[0][0])
+        assert lib.alaya_index_set_valid(ix, back, 1) == 0
+        valid[back] = True
+        flat(base, valid)
+        # 45 rows appended: the last tile record is partial (3045 rows)
+        assert lib.alaya_index_write_rows(ix, n, ptr(extra), len(extra)) == 0, lib.alaya_last_error()
+        assert lib.alaya_index_set_valid(ix, n + 7, 1) == 0  # written rows start invalid
+        rows = np.concatenate([base, extra])
+        valid = np.concatenate([valid, np.zeros(len(extra), bool)])
+        valid[n + 7] = True
+        flat(rows, valid)
+    finally:
+        lib.alaya_index_destroy(ix)
