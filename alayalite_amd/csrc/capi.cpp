@@ -583,7 +583,8 @@ int flat_chunks(alaya_index *ix, int nqg, uint64_t rows) {
 // whole rounds of the CUs best (fewer chunks on ties -- each chunk adds ~32 ln(rows) appends per
 // query).  Every chunk keeps >= 4 records.
 int flat_tiles_chunks(alaya_index *ix, uint64_t nq, uint64_t scan_tiles) {
-  const uint64_t nqg = (nq + alaya_amd::flat_tiles_queries() - 1) / alaya_amd::flat_tiles_queries();
+  const uint64_t qpb = alaya_amd::flat_tiles_queries();
+  const uint64_t nqg = (nq + qpb - 1) / qpb;
   const uint64_t cus = static_cast<uint64_t>(std::max(1, ix->num_cus));
   const uint64_t cap = std::max<uint64_t>(8, std::min<uint64_t>(256, (scan_tiles / 4) / 8 * 8));
   if (nqg * 8 < cus) return static_cast<int>(std::min<uint64_t>(cap, (cus + nqg - 1) / nqg + 7) / 8 * 8);
@@ -650,7 +651,8 @@ void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStr
     q.ablate = 0;
     ix->flat_tau.reserve(p.nq * 4);
     q.tau_out = ix->flat_tau.as<float>();
-    const int nqg = static_cast<int>((p.nq + alaya_amd::flat_tiles_queries() - 1) / alaya_amd::flat_tiles_queries());
+    const int qpb = alaya_amd::flat_tiles_queries();
+    const int nqg = static_cast<int>((p.nq + qpb - 1) / qpb);
     hip_check(alaya_amd::launch_flat_scan(q, nqg * q.n_chunks, s), "flat prescan");
     hip_check(alaya_amd::launch_flat_threshold(q, s), "flat threshold");
     p.tau_init = q.tau_out;
@@ -734,7 +736,8 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
     p.tiles = ix->flat_tiles.as<unsigned char>();
     p.n_scan_tiles = (ix->n + 31) / 32;
     p.tile_step = 1;
-    nqg = static_cast<int>((nq + alaya_amd::flat_tiles_queries() - 1) / alaya_amd::flat_tiles_queries());
+    const int qpb = alaya_amd::flat_tiles_queries();
+    nqg = static_cast<int>((nq + qpb - 1) / qpb);
     chunks = flat_tiles_chunks(ix, nq, p.n_scan_tiles);
   } else {
     nqg = static_cast<int>((nq + 127) / 128);

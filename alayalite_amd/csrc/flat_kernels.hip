@@ -342,6 +342,65 @@ __device__ __forceinline__ void fold_rounds(const FlatParams &p, uint32_t need, 
   }
 }
 
+// fold_rounds with static register indices (an unrolled loop, one fold body per register): the
+// single-role scan folds rarely, and picking the register by value made the compiler copy all 64
+// shortlist registers on every record of the hot loop; the 16 bodies cost code size instead.
+// The single-role scan's shortlist state as plain arrays with static indices only (scalars after
+// SROA): a whole-vector value would be copied at every control-flow join of the hot loop.
+struct TilesLists {
+  float tau[16];
+  uint32_t nonempty;
+  float *ld;     // LDS: this wave's 32 queries x kL shortlist distances (ascending)
+  uint32_t *li;  // and ids
+  uint32_t *cnt;  // LDS: buffered candidates per query
+};
+
+template <int kB>
+__device__ __forceinline__ void fold_rounds_static(const FlatParams &p, uint32_t need, bool last, TilesLists &S,
+                                                   float *bd, uint32_t *bi) {
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  wave_fence();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (!(need & (1u << r))) continue;
+    const int qloc = reg_query(r, h);
+    float L = S.ld[qloc * kL + col];
+    uint32_t Li = S.li[qloc * kL + col];
+    // an append past kB was counted but not stored: the buffer holds min(count, kB)
+    int cr = min(static_cast<int>(S.cnt[qloc]), kB);
+    do {  // one round; the last record repeats until the buffer is empty
+      const int start = max(cr - 32, 0);  // uniform per half
+      float cd = FLT_MAX;
+      uint32_t ci = 0xffffffffu;
+      if (start + col < cr) {
+        cd = bd[qloc * kB + start + col];
+        ci = bi[qloc * kB + start + col];
+      }
+      fold32(L, Li, cd, ci, col);
+      cr = start;
+    } while (last && __builtin_amdgcn_ballot_w64(cr > 0));
+    S.ld[qloc * kL + col] = L;
+    S.li[qloc * kL + col] = Li;
+    if (col == 0) S.cnt[qloc] = static_cast<uint32_t>(cr);
+    if (!__builtin_amdgcn_ballot_w64(cr > 0)) S.nonempty &= ~(1u << r);
+    S.tau[r] = lane31_of_half(L);
+    if (lane == 0 && p.merge_count) atomicAdd(p.merge_count + blockIdx.x, 1u);
+  }
+  wave_fence();
+}
+
+// OR of a per-lane mask over the wave
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  v |= __shfl_xor(v, 1);
+  v |= __shfl_xor(v, 2);
+  v |= __shfl_xor(v, 4);
+  v |= __shfl_xor(v, 8);
+  v |= __shfl_xor(v, 16);
+  v |= __shfl_xor(v, 32);
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 template <int K, bool kSplit>
 __global__ void __launch_bounds__(256) flat_scan_kernel(FlatParams p) {
   static_assert(K % 16 == 0 && K <= 256, "K must be a multiple of 16, at most 256");
@@ -903,33 +962,35 @@ __global__ void flat_tiles_kernel(const float *base, uint64_t n, uint32_t stride
   }
 }
 
-// candidate buffer entries per query: a whole tile of appends above the 32 a due fold may leave
-// (the `need` rule: a buffer holding more than kB - 32 entries is folded before the next tile)
-template <int K>
-constexpr int tiles_buf() { return 64; }
-// tile slots: j (being read) and up to kD - 1 records in flight, as many as the 160 KB leave beside
-// the candidate buffers, at most ALAYA_FLAT_TILES_RING (diagnostics builds; measured: 3 slots as
-// fast as more -- the ring is not what bounds a step)
-#ifndef ALAYA_FLAT_TILES_RING
-#define ALAYA_FLAT_TILES_RING 3
+// Candidate buffers: kB = 32 entries per query; an append that finds its buffer full is retried
+// after that buffer is folded -- exact for any data and any kB.  The shortlists (32 entries per
+// query) live in LDS beside them, the thresholds in registers.
+constexpr int kTilesBuf = 32;
+constexpr int kTilesWaveLds = 32 * (kTilesBuf * 8 + kL * 8 + 4);  // buffers, shortlists, counts
+// Records per barrier group: the block meets once per kG records (the pieces of group g landed,
+// group g - 1 read by every wave, its slots refilled with group g + 1), so a wave's candidate work
+// on one record overlaps the other waves' contractions instead of holding all of them at a
+// per-record barrier.  2 kG slots (two groups) beside the 8 waves' candidate buffers in 160 KB,
+// at most ALAYA_FLAT_TILES_GROUP (diagnostics builds).
+#ifndef ALAYA_FLAT_TILES_GROUP
+#define ALAYA_FLAT_TILES_GROUP 4
 #endif
 template <int K>
-constexpr int tiles_ring() {
-  constexpr int fit = static_cast<int>((160 * 1024 - 8 * 32 * tiles_buf<K>() * 8) / (K / 16 * 1024 + 256));
-  return fit < ALAYA_FLAT_TILES_RING ? fit : ALAYA_FLAT_TILES_RING;
+constexpr int tiles_group() {
+  constexpr int fit = static_cast<int>((160 * 1024 - 8 * kTilesWaveLds) / (2 * (K / 16 * 1024 + 256)));
+  return fit < ALAYA_FLAT_TILES_GROUP ? fit : ALAYA_FLAT_TILES_GROUP;
 }
 template <int K>
 constexpr size_t tiles_lds() {
-  return static_cast<size_t>(tiles_ring<K>()) * tiles_rec<K>() + static_cast<size_t>(8) * 32 * tiles_buf<K>() * 8;
+  return static_cast<size_t>(2 * tiles_group<K>()) * tiles_rec<K>() + static_cast<size_t>(8) * kTilesWaveLds;
 }
 template <int K>
 constexpr bool tiles_fits() {
-  return tiles_lds<K>() <= 160 * 1024 && tiles_buf<K>() >= 2 * kTile && tiles_ring<K>() >= 2;
+  return tiles_lds<K>() <= 160 * 1024 && tiles_group<K>() >= 1;
 }
-
 static_assert(tiles_fits<32>() && tiles_fits<64>() && tiles_fits<96>() && tiles_fits<128>() && tiles_fits<160>() &&
                   tiles_fits<192>() && tiles_fits<224>(),
-              "single-role f16 scan: tile ring / candidate buffers");
+              "single-role f16 scan: tile groups / candidate buffers");
 
 // this wave's DMA pieces of one record: pieces w, w + 8, ... of K/16 fragment pieces (16 B per lane)
 // and the tail (4 B per lane)
@@ -955,19 +1016,26 @@ __device__ __forceinline__ void tiles_issue(const unsigned char *src, unsigned c
 template <int K, bool kMin>
 __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   static_assert(K % 16 == 0 && K <= 224, "narrow rows");
+  constexpr int kW = 8;
   constexpr int kSteps = K / 16;
   constexpr int kRec = tiles_rec<K>();
-  constexpr int kB = tiles_buf<K>();
-  constexpr int kD = tiles_ring<K>();
+  constexpr int kB = kTilesBuf;
+  constexpr int kG = tiles_group<K>();
+  constexpr int kD = 2 * kG;
+  constexpr bool kPre = true;  // fold before an overflowing append (kB = 32)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar branches on it
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
-  float *bd = reinterpret_cast<float *>(smem + kD * kRec) + wave * 32 * kB * 2;  // 32 queries x kB
+  unsigned char *wl = smem + kD * kRec + wave * kTilesWaveLds;  // this wave's LDS: buffers, lists, counts
+  float *bd = reinterpret_cast<float *>(wl);                        // 32 queries x kB
   uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
+  float *ldL = reinterpret_cast<float *>(bi + 32 * kB);            // 32 queries x kL
+  uint32_t *liL = reinterpret_cast<uint32_t *>(ldL + 32 * kL);
+  uint32_t *cntL = liL + 32 * kL;                                   // 32
 
   // XCD-aware: the query groups of a chunk are consecutive multiples of 8 apart (one XCD)
-  const int nqg = static_cast<int>((p.nq + 255) / 256);
+  const int nqg = static_cast<int>((p.nq + 32 * kW - 1) / (32 * kW));
   const int b = blockIdx.x;
   const int qg = (b / 8) % nqg;
   const int chunk = (b % 8) + 8 * (b / (8 * nqg));
@@ -976,7 +1044,7 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   const uint64_t j0 = chunk * per;
   const uint64_t j1 = min(p.n_scan_tiles, j0 + per);
   const int ntiles = j1 > j0 ? static_cast<int>(j1 - j0) : 0;
-  const uint64_t q0 = static_cast<uint64_t>(qg) * 256 + wave * 32;
+  const uint64_t q0 = static_cast<uint64_t>(qg) * (32 * kW) + wave * 32;
 
   // A fragments of the wave's 32 queries, each scaled by its own 2^t (the ws scan's producer code).
   // The loads are unconditional (a clamped row and column, the value selected afterwards): a load
@@ -1012,44 +1080,58 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   f32xN<16> m2u;
 #pragma unroll
   for (int r = 0; r < 16; ++r) m2u[r] = ldexpf(-2.0f, -(p.base_exp + __shfl(t_own, reg_query(r, h))));
-  ShortlistsT<16> S;
-  init_shortlists<16, 0>(p, q0, h, S);
+  TilesLists S;
+  S.nonempty = 0;
+  S.ld = ldL;
+  S.li = liL;
+  S.cnt = cntL;
+  if (!kMin) {
+    for (int e = lane; e < 32 * kL; e += 64) {
+      ldL[e] = FLT_MAX;
+      liL[e] = 0xffffffffu;
+    }
+    if (lane < 32) cntL[lane] = 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint64_t qi = q0 + reg_query(r, h);
+    S.tau[r] = qi < p.nq ? (p.tau_init ? p.tau_init[qi] : FLT_MAX) : -FLT_MAX;  // empty slots: no candidates
+  }
   f32xN<16> rmin;  // kMin: running minimum of register r's query over the group
 #pragma unroll
   for (int r = 0; r < 16; ++r) rmin[r] = __builtin_inff();
 
   const unsigned char *recs = p.tiles;
   auto rec_of = [&](int jj) { return recs + (j0 + jj) * p.tile_step * kRec; };
-  // pieces this wave issues per record (wave-uniform): the vmcnt count of one record
-  const int pw = wave < kSteps + 1 ? (kSteps + 1 - wave + 7) / 8 : 0;
+  // record t lives in slot (t / kG % 2) kG + t % kG: group g in one half of the ring, g + 1 in the other
+  auto slot_of = [&](int t) { return smem + (((t / kG) & 1) * kG + t % kG) * kRec; };
 #pragma unroll
-  for (int jj = 0; jj < kD - 1; ++jj)
-    if (jj < ntiles) tiles_issue<K>(rec_of(jj), smem + jj * kRec, wave, lane);
+  for (int jj = 0; jj < kG; ++jj)
+    if (jj < ntiles) tiles_issue<K>(rec_of(jj), slot_of(jj), wave, lane);
   // diagnostics (p.merge_count): per-wave s_memtime totals of the wait + barrier, the contraction
   // and threshold test, and the candidate handling; p.ablate 1 skips the candidate handling, 3 the
   // contraction too (the DMA ring and the barriers alone)
   const bool diag = p.merge_count != nullptr;
   uint64_t t_wait = 0, t_mm = 0, t_cand = 0, sink = 0;
+  uint32_t n_ctile = 0, n_app = 0;  // diagnostics: records with a candidate, appended candidates
   const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
   for (int jj = 0; jj < ntiles; ++jj) {
     const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-    // this wave's pieces of tile jj have landed: at most the pieces of tiles jj + 1 .. jj + kD - 2
-    // stay in flight (and its LDS reads of tile jj - 1 are done before the barrier lets that slot
-    // be refilled)
-    asm volatile("" ::: "memory");
-    if (jj + kD - 2 < ntiles) {
-      if (pw == 2) __builtin_amdgcn_s_waitcnt(0x70 | (2 * (kD - 2)));
-      else __builtin_amdgcn_s_waitcnt(0x70 | (kD - 2));
-    } else {
-      __builtin_amdgcn_s_waitcnt(0x70);
+    if (jj % kG == 0) {
+      // group start: this wave's pieces of the group have landed and its LDS reads of the previous
+      // group are done; after the barrier every wave's are, and the previous group's slots take
+      // the next group
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0x70);  // vmcnt(0) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < kG; ++i)
+        if (jj + kG + i < ntiles) tiles_issue<K>(rec_of(jj + kG + i), slot_of(jj + kG + i), wave, lane);
     }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
     const uint64_t tm = diag ? __builtin_amdgcn_s_memtime() : 0;
     if (diag) t_wait += tm - tw;
-    const int slot = jj % kD;
-    if (jj + kD - 1 < ntiles) tiles_issue<K>(rec_of(jj + kD - 1), smem + ((jj + kD - 1) % kD) * kRec, wave, lane);
-    const unsigned char *tl = smem + slot * kRec;
+    const unsigned char *tl = slot_of(jj);
     if (p.ablate == 3) continue;
     // every B fragment of the tile in flight at once (one LDS latency, not one per MFMA pair)
     f16x8 bf[kSteps];
@@ -1081,42 +1163,65 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
       sink += any;
       continue;
     }
-    // Candidates are rare once the prescan threshold is in (~10 per query and chunk), so the tile
-    // test above keeps only their union; a tile that has one recomputes each register's lane mask
-    // (the asm keeps the compiler from holding 16 masks in SGPRs across the common path), appends,
-    // and folds a buffer that could overflow on the next tile (more than kB - 32 entries).  The
-    // last tile drains every buffer.
-    uint32_t need = 0;
+    // Candidates are rare once the prescan threshold is in (~10 per query and chunk): a record with
+    // one builds each lane's 16-bit pass mask, and only the passing (lane, register) pairs do any
+    // work -- a buffer slot from an LDS atomic add on the query's count, the (distance, id) store.
+    // An append that finds its buffer full (kB = 32) is retried after the buffers it overfilled
+    // are folded (against their tightened thresholds).  The last record drains every buffer.
     if (any) {
+      if (diag) ++n_ctile;
+      uint32_t pm = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float d = dv[r];
-        asm volatile("" : "+v"(d));
-        const uint64_t m = __builtin_amdgcn_fcmpf(d, S.tau[r], 4);
-        if (!m) continue;
-        const uint32_t lo = static_cast<uint32_t>(m), hi = static_cast<uint32_t>(m >> 32);
-        const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u))) -
-                          (h ? __popc(lo) : 0);
-        const int cr = S.cnt[r];
-        if ((m >> lane) & 1ull) {
-          const int at = reg_query(r, h) * kB + cr + below;
-          bd[at] = d;
-          bi[at] = static_cast<uint32_t>(rid);
+      for (int r = 0; r < 16; ++r) pm |= dv[r] < S.tau[r] ? (1u << r) : 0u;
+      for (;;) {
+        uint32_t ne = 0, over = 0;
+        for (uint32_t m = pm; m; m &= m - 1) {
+          const int r = __builtin_ctz(m);
+          float d = dv[0];
+#pragma unroll
+          for (int r2 = 1; r2 < 16; ++r2) d = r2 == r ? dv[r2] : d;
+          const int q = reg_query(r, h);
+          const uint32_t pos = atomicAdd(&cntL[q], 1u);
+          if (pos < static_cast<uint32_t>(kB)) {
+            bd[q * kB + pos] = d;
+            bi[q * kB + pos] = static_cast<uint32_t>(rid);
+            ne |= 1u << r;
+            if (diag) ++n_app;
+          } else {
+            over |= 1u << r;
+          }
         }
-        const int nc = cr + (h ? __popc(hi) : __popc(lo));
-        S.cnt[r] = nc;
-        S.nonempty |= 1u << r;
-        if (__builtin_amdgcn_ballot_w64(nc > kB - kTile)) need |= 1u << r;
+        (void)ne;
+        if (!__builtin_amdgcn_ballot_w64(over != 0u)) break;  // the common case: no buffer overflowed
+        const uint32_t fold = wave_or(over);
+        if (p.ablate == 4) {  // diagnostics: overflowing candidates dropped instead of folded
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if ((fold & (1u << r)) && col == 0) cntL[reg_query(r, h)] = 0u;
+          break;
+        }
+        fold_rounds_static<kB>(p, fold, false, S, bd, bi);
+        // retry the overflowed candidates that still pass the tightened thresholds
+        uint32_t retry = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          retry |= ((over & (1u << r)) && dv[r] < S.tau[r]) ? (1u << r) : 0u;
+        pm = retry;
       }
     }
-    if (last) need |= S.nonempty;
-    if (p.ablate == 4) {  // diagnostics: appends only, buffers dropped instead of folded
+    if (last && p.ablate != 4) {
+      // drain: every register with a buffered candidate in either half (counts from LDS)
+      const int c0 = static_cast<int>(cntL[col]);  // lane l: query l & 31
+      uint32_t ne = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (need & (1u << r)) S.cnt[r] = 0;
-      need = 0;
+      for (int r = 0; r < 16; ++r) {
+        const int qa = reg_query(r, 0), qb = reg_query(r, 1);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(c0 > 0 && (col == qa || col == qb));
+        ne |= m ? (1u << r) : 0u;
+      }
+      S.nonempty = ne;
+      if (ne) fold_rounds_static<kB>(p, ne, true, S, bd, bi);
     }
-    if (need) fold_rounds<kB, 16, 0>(p, need, last, S, bd, bi);
     if (diag) t_cand += __builtin_amdgcn_s_memtime() - tc;
   }
   if constexpr (kMin) {
@@ -1135,13 +1240,25 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
     return;
   }
   if (diag && lane == 0) {  // diagnostics rows (tools/ab_flat.py --diag): total, wait, contraction, candidates
-    unsigned long long *st = reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * 8 + wave) * 4;
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(p.merge_count + 4096) + (blockIdx.x * kW + wave) * 8;
     st[0] = __builtin_amdgcn_s_memtime() - t_start;
     st[1] = t_wait;
     st[2] = t_mm;
     st[3] = t_cand + (sink == 0xffffffffffffffffull ? 1 : 0);
+    st[4] = n_ctile;
+    st[5] = n_app;
+    st[6] = ntiles;
+    st[7] = 0;
   }
-  store_shortlists<16, 0>(p, q0, chunk, S);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint64_t qi = q0 + reg_query(r, h);
+    if (qi < p.nq) {
+      const uint64_t o = (static_cast<uint64_t>(chunk) * p.nq + qi) * kL + col;
+      p.cand_d[o] = ldL[reg_query(r, h) * kL + col];
+      p.cand_i[o] = liL[reg_query(r, h) * kL + col];
+    }
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1867,11 +1984,11 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s) {
     switch (p.stride) {
 #define ALAYA_TILES(K)                                                                                          \
   case K:                                                                                                       \
-    if (p.tau_out)                                                                                             \
+    if (p.tau_out)                                                                                              \
       hipLaunchKernelGGL((flat_scan_tiles_kernel<K, true>), dim3(blocks), dim3(512),                           \
-                         static_cast<size_t>(tiles_ring<K>()) * tiles_rec<K>(), s, p);                        \
+                         (static_cast<size_t>(2 * tiles_group<K>()) * tiles_rec<K>()), s, p);                 \
     else                                                                                                        \
-      hipLaunchKernelGGL((flat_scan_tiles_kernel<K, false>), dim3(blocks), dim3(512), tiles_lds<K>(), s, p);   \
+      hipLaunchKernelGGL((flat_scan_tiles_kernel<K, false>), dim3(blocks), dim3(512), (tiles_lds<K>()), s, p); \
     break;
       ALAYA_TILES(32) ALAYA_TILES(64) ALAYA_TILES(96) ALAYA_TILES(128) ALAYA_TILES(160) ALAYA_TILES(192)
       ALAYA_TILES(224)

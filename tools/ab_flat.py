@@ -71,7 +71,7 @@ def main():
                       f"{nq / ms * 1e3:,.0f} QPS  ids-hash {h}  flagged {int(fl.sum().item())}  "
                       f"contraction {dev.flat_contraction()}", flush=True)
                 for ab in [int(x) for x in args.diag.split(",") if x != ""]:
-                    mc = torch.zeros((4096 + 2 * 4 * 4096 * 4,), dtype=torch.int32, device="cuda")
+                    mc = torch.zeros((4096 + 2 * 8 * 16384 * 8,), dtype=torch.int32, device="cuda")
                     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     a.record(st)
                     dev.flat_diag(qd.data_ptr(), nq, args.k, ab, ids.data_ptr(), dd.data_ptr(), fl.data_ptr(),
@@ -79,14 +79,16 @@ def main():
                     b.record(st)
                     torch.cuda.synchronize()
                     m = mc.cpu().numpy()
-                    rows = m[4096:].view(np.uint64).reshape(-1, 4).astype(np.float64)
+                    rows = m[4096:].view(np.uint64).reshape(-1, 8).astype(np.float64)
                     rows = rows[rows[:, 0] > 0]
                     msg = ""
                     if len(rows):
                         tot = rows[:, 0].mean()
                         msg = (f"  per-wave ticks {tot:.0f}: wait+barrier {rows[:, 1].mean() / tot:.2f} "
                                f"contraction+test {rows[:, 2].mean() / tot:.2f} candidates {rows[:, 3].mean() / tot:.2f} "
-                               f"(max-wave candidates {rows[:, 3].max() / tot:.2f})")
+                               f"(max-wave candidates {rows[:, 3].max() / tot:.2f}); records with a candidate "
+                               f"{rows[:, 4].mean():.1f} of {rows[:, 6].mean():.1f}, candidates {rows[:, 5].mean():.1f} "
+                               f"per wave")
                     nz = m[:4096][m[:4096] > 0]
                     print(f"   diag ablate={ab}: {a.elapsed_time(b):.3f} ms (scan + prescan, no merge)  fold rounds/block "
                           f"{nz.mean() if len(nz) else 0:.1f}{msg}", flush=True)
