@@ -45,6 +45,9 @@ def main(src, dst, mode="hnsw"):
     if mode == "flat":  # the base and the queries read once, the chunk shortlists written once
         cf = cfg["config"]
         alg = 4.0 * cf["dim"] * (cf["n_base"] + cf["n_queries"]) + 4.0 * cf["n_base"]
+        if any("tiles" in n for n in names):  # the single-role scan reads the f16 tile records instead
+            k = (cf["dim"] + 31) // 32 * 32
+            alg = (cf["n_base"] + 31) // 32 * (k // 16 * 1024 + 256) + 4.0 * cf["dim"] * cf["n_queries"]
     else:
         alg = cfg["roofline"]["algorithmic_bytes_per_launch"]
         if cfg.get("dtype") == "u8+f32":  # SQ8: the profiled kernel is the search; the rerank's f32 rows
