@@ -43,6 +43,7 @@ struct FlatParams {
                                // (launch_flat_tiles), rows already scaled by 2^base_exp
   uint64_t n_scan_tiles;       // records the scan visits: 0, tile_step, 2 tile_step, ... (split over the chunks)
   uint32_t tile_step;          // 1 = every record; the prescan's sample takes every tile_step-th
+  uint64_t *tiles_buf;         // its candidate buffers: blocks x flat_tiles_queries() x flat_tiles_buf() entries
 };
 
 int flat_shortlist();
@@ -65,8 +66,9 @@ hipError_t launch_flat_scan(const FlatParams &p, int blocks, hipStream_t s);
 size_t flat_tiles_bytes(uint32_t stride, uint64_t n);
 hipError_t launch_flat_tiles(const float *base, uint64_t n, uint32_t stride, const float *norms, const uint32_t *valid,
                              int base_exp, unsigned char *out, hipStream_t s);
-// queries per block of the single-role f16 scan
+// queries per block of the single-role f16 scan, and candidate buffer entries per query
 int flat_tiles_queries();
+int flat_tiles_buf();
 hipError_t launch_flat_merge(const FlatParams &p, hipStream_t s);
 hipError_t launch_flat_threshold(const FlatParams &p, hipStream_t s);
 

@@ -357,9 +357,11 @@ struct TilesLists {
 
 template <int kB>
 __device__ __forceinline__ void fold_rounds_static(const FlatParams &p, uint32_t need, bool last, TilesLists &S,
-                                                   float *bd, uint32_t *bi) {
+                                                   const uint64_t *gb) {
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
+  // this wave's appends (global stores) have completed before it reads them back, past L1
+  __builtin_amdgcn_s_waitcnt(0x70);  // vmcnt(0) lgkmcnt(0)
   wave_fence();
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -374,8 +376,9 @@ __device__ __forceinline__ void fold_rounds_static(const FlatParams &p, uint32_t
       float cd = FLT_MAX;
       uint32_t ci = 0xffffffffu;
       if (start + col < cr) {
-        cd = bd[qloc * kB + start + col];
-        ci = bi[qloc * kB + start + col];
+        const uint64_t v = __hip_atomic_load(gb + qloc * kB + start + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cd = __uint_as_float(static_cast<uint32_t>(v));
+        ci = static_cast<uint32_t>(v >> 32);
       }
       fold32(L, Li, cd, ci, col);
       cr = start;
@@ -901,16 +904,18 @@ __global__ void __launch_bounds__(256 * (1 + kCons)) flat_scan_ws_kernel(FlatPar
 // in the single-pass contraction).  The warp-specialised scan above converts every f32 row tile
 // to f16 in each of the 8 blocks that scan it and hands each 32x32 contraction from a producer to
 // a consumer through LDS flags; the tile records below are converted once per base (cached on the
-// index) and laid out as the MFMA's B fragments in lane order, so a block stages a tile with one
+// index) and laid out as the MFMA's B fragments in lane order, so a block stages a record with one
 // lane-linear global->LDS DMA per 1 KB piece and every wave reads its fragments with conflict-free
 // ds_read_b128.  512 threads = 8 waves (two per SIMD), each holding 32 queries as A fragments,
-// 256 queries per block sharing every staged tile; each wave contracts the tile (K/16 MFMAs),
+// 256 queries per block sharing every staged record; each wave contracts the record (K/16 MFMAs),
 // forms the 1,024 approximate distances and tests them against its queries' thresholds in one
-// pass, and only a tile with a candidate (or a due fold) enters tile_candidates -- the same
-// appends, fold rounds and register shortlists as the other scans, so the merge and its error
-// bound (the single pass's) are unchanged.  One raw s_barrier per tile orders the ring: after it,
-// every wave's pieces of tile j have landed (each wave waited for its own DMA) and every wave has
-// finished tile j - 1, whose slot is then refilled with tile j + kD - 1.
+// pass, and only a record with a candidate enters the append path (LDS atomic slots in 32-entry
+// buffers, folds into LDS-resident shortlists only on overflow and at the end), so the merge and
+// its error bound (the single pass's) are those of the other scans.  One raw s_barrier per group
+// of kG records orders the slots: after it, every wave's pieces of the group have landed (each
+// wave waited for its own DMA) and every wave has finished the previous group, whose slots are
+// then refilled with the next.  A prescan launch of the same kernel (kMin) over a sample of the
+// records gives every query a starting threshold (flat_group_threshold_kernel).
 // --------------------------------------------------------------------------------------------
 // Tile record T (rows 32T .. 32T+31): K/16 pieces of 64 lanes x 8 f16 -- lane l: row 32T + (l & 31),
 // k = (l >> 5) K/2 + 8 st + j, the k map of the other scans' A fragments -- each element
@@ -962,11 +967,13 @@ __global__ void flat_tiles_kernel(const float *base, uint64_t n, uint32_t stride
   }
 }
 
-// Candidate buffers: kB = 32 entries per query; an append that finds its buffer full is retried
-// after that buffer is folded -- exact for any data and any kB.  The shortlists (32 entries per
-// query) live in LDS beside them, the thresholds in registers.
+// Candidate buffers: kB = 32 entries per query in global memory (L2: p.tiles_buf, written with
+// plain stores, read back past L1 by the rare folds); an append that finds its buffer full is
+// retried after that buffer is folded -- exact for any data and any kB.  The shortlists (32
+// entries per query) and the counts live in LDS, the thresholds in registers; the LDS the buffers
+// would take holds records instead (barrier groups of up to 4 records).
 constexpr int kTilesBuf = 32;
-constexpr int kTilesWaveLds = 32 * (kTilesBuf * 8 + kL * 8 + 4);  // buffers, shortlists, counts
+constexpr int kTilesWaveLds = 32 * (kL * 8 + 4);  // shortlists, counts
 // Records per barrier group: the block meets once per kG records (the pieces of group g landed,
 // group g - 1 read by every wave, its slots refilled with group g + 1), so a wave's candidate work
 // on one record overlaps the other waves' contractions instead of holding all of them at a
@@ -1027,10 +1034,8 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar branches on it
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
-  unsigned char *wl = smem + kD * kRec + wave * kTilesWaveLds;  // this wave's LDS: buffers, lists, counts
-  float *bd = reinterpret_cast<float *>(wl);                        // 32 queries x kB
-  uint32_t *bi = reinterpret_cast<uint32_t *>(bd + 32 * kB);
-  float *ldL = reinterpret_cast<float *>(bi + 32 * kB);            // 32 queries x kL
+  unsigned char *wl = smem + kD * kRec + wave * kTilesWaveLds;  // this wave's LDS: lists, counts
+  float *ldL = reinterpret_cast<float *>(wl);                       // 32 queries x kL
   uint32_t *liL = reinterpret_cast<uint32_t *>(ldL + 32 * kL);
   uint32_t *cntL = liL + 32 * kL;                                   // 32
 
@@ -1045,6 +1050,8 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   const uint64_t j1 = min(p.n_scan_tiles, j0 + per);
   const int ntiles = j1 > j0 ? static_cast<int>(j1 - j0) : 0;
   const uint64_t q0 = static_cast<uint64_t>(qg) * (32 * kW) + wave * 32;
+  // this wave's candidate buffers: 32 queries x kB (distance bits | id << 32)
+  uint64_t *gb = kMin ? nullptr : p.tiles_buf + (static_cast<uint64_t>(blockIdx.x) * kW + wave) * 32 * kB;
 
   // A fragments of the wave's 32 queries, each scaled by its own 2^t (the ws scan's producer code).
   // The loads are unconditional (a clamped row and column, the value selected afterwards): a load
@@ -1183,8 +1190,7 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
           const int q = reg_query(r, h);
           const uint32_t pos = atomicAdd(&cntL[q], 1u);
           if (pos < static_cast<uint32_t>(kB)) {
-            bd[q * kB + pos] = d;
-            bi[q * kB + pos] = static_cast<uint32_t>(rid);
+            gb[q * kB + pos] = static_cast<uint64_t>(__float_as_uint(d)) | (static_cast<uint64_t>(rid) << 32);
             ne |= 1u << r;
             if (diag) ++n_app;
           } else {
@@ -1200,7 +1206,7 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
             if ((fold & (1u << r)) && col == 0) cntL[reg_query(r, h)] = 0u;
           break;
         }
-        fold_rounds_static<kB>(p, fold, false, S, bd, bi);
+        fold_rounds_static<kB>(p, fold, false, S, gb);
         // retry the overflowed candidates that still pass the tightened thresholds
         uint32_t retry = 0;
 #pragma unroll
@@ -1220,7 +1226,7 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
         ne |= m ? (1u << r) : 0u;
       }
       S.nonempty = ne;
-      if (ne) fold_rounds_static<kB>(p, ne, true, S, bd, bi);
+      if (ne) fold_rounds_static<kB>(p, ne, true, S, gb);
     }
     if (diag) t_cand += __builtin_amdgcn_s_memtime() - tc;
   }
@@ -1957,6 +1963,7 @@ size_t flat_tiles_bytes(uint32_t stride, uint64_t n) {
 }
 
 int flat_tiles_queries() { return 256; }
+int flat_tiles_buf() { return kTilesBuf; }
 
 hipError_t launch_flat_tiles(const float *base, uint64_t n, uint32_t stride, const float *norms, const uint32_t *valid,
                              int base_exp, unsigned char *out, hipStream_t s) {
