@@ -120,7 +120,7 @@ struct alaya_index {
   bool norms_ready = false;
   // single-role f16 flat scan: the base's tile records (alaya_amd::launch_flat_tiles), built at the
   // first flat search after any change to the rows, their count or the validity bitmap
-  DevBuf flat_tiles, tiles_cand;  // the records; the scan's per-launch candidate buffers
+  DevBuf flat_tiles, tiles_cand, tiles_qexp;  // the records; the scan's candidate buffers, query scales
   bool tiles_ready = false;
   int tiles_exp = 0;
   float max_norm = 0.f;
@@ -741,6 +741,8 @@ alaya_amd::FlatParams flat_params(alaya_index *ix, const float *d_q, uint64_t nq
     chunks = flat_tiles_chunks(ix, nq, p.n_scan_tiles);
     ix->tiles_cand.reserve(static_cast<size_t>(nqg) * chunks * qpb * alaya_amd::flat_tiles_buf() * 8);
     p.tiles_buf = ix->tiles_cand.as<uint64_t>();
+    ix->tiles_qexp.reserve(nq * 4);
+    p.tiles_qexp = ix->tiles_qexp.as<int>();
   } else {
     nqg = static_cast<int>((nq + 127) / 128);
     chunks = flat_chunks(ix, nqg, ix->n);

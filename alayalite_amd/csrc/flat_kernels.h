@@ -44,6 +44,7 @@ struct FlatParams {
   uint64_t n_scan_tiles;       // records the scan visits: 0, tile_step, 2 tile_step, ... (split over the chunks)
   uint32_t tile_step;          // 1 = every record; the prescan's sample takes every tile_step-th
   uint64_t *tiles_buf;         // its candidate buffers: blocks x flat_tiles_queries() x flat_tiles_buf() entries
+  int *tiles_qexp;             // its scale exponent t per query (one per wave of 32 queries), for the merge's bound
 };
 
 int flat_shortlist();

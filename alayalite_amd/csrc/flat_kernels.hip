@@ -987,13 +987,14 @@ constexpr int tiles_group() {
   constexpr int fit = static_cast<int>((160 * 1024 - 8 * kTilesWaveLds) / (2 * (K / 16 * 1024 + 256)));
   return fit < ALAYA_FLAT_TILES_GROUP ? fit : ALAYA_FLAT_TILES_GROUP;
 }
+// dynamic LDS of a launch: the record slots (the lists and counts are a static LDS object)
 template <int K>
 constexpr size_t tiles_lds() {
-  return static_cast<size_t>(2 * tiles_group<K>()) * tiles_rec<K>() + static_cast<size_t>(8) * kTilesWaveLds;
+  return static_cast<size_t>(2 * tiles_group<K>()) * tiles_rec<K>();
 }
 template <int K>
 constexpr bool tiles_fits() {
-  return tiles_lds<K>() <= 160 * 1024 && tiles_group<K>() >= 1;
+  return tiles_lds<K>() + static_cast<size_t>(8) * kTilesWaveLds <= 160 * 1024 && tiles_group<K>() >= 1;
 }
 static_assert(tiles_fits<32>() && tiles_fits<64>() && tiles_fits<96>() && tiles_fits<128>() && tiles_fits<160>() &&
                   tiles_fits<192>() && tiles_fits<224>(),
@@ -1034,7 +1035,10 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar branches on it
   const int lane = lane_id();
   const int h = lane >> 5, col = lane & 31;
-  unsigned char *wl = smem + kD * kRec + wave * kTilesWaveLds;  // this wave's LDS: lists, counts
+  // the lists and counts in an LDS object of their own: the compiler then knows the record DMA
+  // (into smem) cannot alias them and does not drain it (vmcnt(0)) before each append's atomic
+  __shared__ __attribute__((aligned(16))) unsigned char lists_lds[kMin ? 16 : 8 * kTilesWaveLds];
+  unsigned char *wl = lists_lds + (kMin ? 0 : wave * kTilesWaveLds);  // this wave's lists, counts
   float *ldL = reinterpret_cast<float *>(wl);                       // 32 queries x kL
   uint32_t *liL = reinterpret_cast<uint32_t *>(ldL + 32 * kL);
   uint32_t *cntL = liL + 32 * kL;                                   // 32
@@ -1076,17 +1080,19 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < kSteps * 8; ++i) mx = fmaxf(mx, fabsf(x[i]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    // one scale 2^t for the wave's 32 queries, from their largest element (every scaled operand stays
+    // below 2^15); flat_merge_kernel's bound takes this t from p.tiles_qexp
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     t_own = f16_exp(mx);
+    if (!kMin && p.tiles_qexp && qok && h == 0) p.tiles_qexp[qi] = t_own;
 #pragma unroll
     for (int s = 0; s < kSteps; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) aq[s][j] = static_cast<_Float16>(ldexpf(x[8 * s + j], t_own));
   }
-  // -2 x the scale-back 2^-(s + t) of register r's query: a = fma(m2u, C~, |b|^2)
-  f32xN<16> m2u;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) m2u[r] = ldexpf(-2.0f, -(p.base_exp + __shfl(t_own, reg_query(r, h))));
+  // -2 x the scale-back 2^-(s + t), one value for the wave: a = fma(m2s, C~, |b|^2)
+  const float m2s = ldexpf(-2.0f, -(p.base_exp + t_own));
   TilesLists S;
   S.nonempty = 0;
   S.ld = ldL;
@@ -1104,6 +1110,10 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
     const uint64_t qi = q0 + reg_query(r, h);
     S.tau[r] = qi < p.nq ? (p.tau_init ? p.tau_init[qi] : FLT_MAX) : -FLT_MAX;  // empty slots: no candidates
   }
+  // the thresholds' loads complete here, not at their first use inside the loop (a vmcnt(0) there
+  // would also wait out the record DMA in flight on every record)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(S.tau[r]));
   f32xN<16> rmin;  // kMin: running minimum of register r's query over the group
 #pragma unroll
   for (int r = 0; r < 16; ++r) rmin[r] = __builtin_inff();
@@ -1122,9 +1132,18 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
   uint64_t t_wait = 0, t_mm = 0, t_cand = 0, sink = 0;
   uint32_t n_ctile = 0, n_app = 0;  // diagnostics: records with a candidate, appended candidates
   const uint64_t t_start = diag ? __builtin_amdgcn_s_memtime() : 0;
-  for (int jj = 0; jj < ntiles; ++jj) {
+  // Software pipeline (the scan proper): record jj's MFMAs are issued between the distance forms
+  // and threshold compares of record jj - 1, so the matrix pipe and the VALU overlap inside the
+  // wave; record jj - 1's candidates follow.  cp/bnp/ridp: the previous record (|b|^2 = +inf
+  // before the first, so it yields no candidate).
+  f32x16 cp = {};
+  float bnp = __builtin_inff();
+  uint64_t ridp = 0;
+  for (int jj = 0; jj <= ntiles; ++jj) {
+    // the extra trip (jj == ntiles) only finishes the last record: its test, candidates and drain
+    if (jj == ntiles && (kMin || ntiles == 0)) break;
     const uint64_t tw = diag ? __builtin_amdgcn_s_memtime() : 0;
-    if (jj % kG == 0) {
+    if (jj % kG == 0 && jj < ntiles) {
       // group start: this wave's pieces of the group have landed and its LDS reads of the previous
       // group are done; after the barrier every wave's are, and the previous group's slots take
       // the next group
@@ -1138,9 +1157,11 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
     }
     const uint64_t tm = diag ? __builtin_amdgcn_s_memtime() : 0;
     if (diag) t_wait += tm - tw;
-    const unsigned char *tl = slot_of(jj);
+    const unsigned char *tl = slot_of(jj < ntiles ? jj : 0);
     if (p.ablate == 3) continue;
     // every B fragment of the tile in flight at once (one LDS latency, not one per MFMA pair)
+    // (the extra trip reads a settled slot and contracts it unused: no branch splits the block
+    // that interleaves these MFMAs with the previous record's compares)
     f16x8 bf[kSteps];
 #pragma unroll
     for (int st = 0; st < kSteps; ++st) bf[st] = *reinterpret_cast<const f16x8 *>(tl + st * 1024 + lane * 16);
@@ -1148,22 +1169,28 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
     // all reads issued before the first MFMA waits on one (K <= 128; wider rows would spill)
     if constexpr (kSteps <= 8) __builtin_amdgcn_sched_barrier(0);
     f32x16 c = {};
+    // the previous record's distances and compares, interleaved with this record's MFMAs
+    f32xN<16> dv;
+    uint64_t any = 0;
+    if constexpr (!kMin) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dv[r] = fmaf(m2s, cp[r], bnp);
+        any |= __builtin_amdgcn_fcmpf(dv[r], S.tau[r], 4);
+      }
+    }
 #pragma unroll
     for (int st = 0; st < kSteps; ++st) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(aq[st], bf[st], c, 0, 0, 0);
     if constexpr (kMin) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) rmin[r] = fminf(rmin[r], fmaf(m2u[r], c[r], bn));
+      for (int r = 0; r < 16; ++r) rmin[r] = fminf(rmin[r], fmaf(m2s, c[r], bn));
       continue;
     }
-    const uint64_t rid = ((j0 + jj) * p.tile_step) * 32 + col;
-    f32xN<16> dv;
-    uint64_t any = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      dv[r] = fmaf(m2u[r], c[r], bn);
-      any |= __builtin_amdgcn_fcmpf(dv[r], S.tau[r], 4);
-    }
-    const bool last = jj == ntiles - 1;
+    const uint64_t rid = ridp;  // the previous record's rows
+    cp = c;
+    bnp = bn;
+    ridp = ((j0 + jj) * p.tile_step) * 32 + col;
+    const bool last = jj == ntiles;
     const uint64_t tc = diag ? __builtin_amdgcn_s_memtime() : 0;
     if (diag) t_mm += tc - tm;
     if (p.ablate == 1) {
@@ -1188,7 +1215,13 @@ __global__ void __launch_bounds__(512) flat_scan_tiles_kernel(FlatParams p) {
 #pragma unroll
           for (int r2 = 1; r2 < 16; ++r2) d = r2 == r ? dv[r2] : d;
           const int q = reg_query(r, h);
-          const uint32_t pos = atomicAdd(&cntL[q], 1u);
+          // the slot: an LDS atomic add on the query's count, in asm -- the compiler cannot tell this
+          // address from the record DMA's and would otherwise drain that DMA (vmcnt(0)) first
+          uint32_t pos;
+          const uint32_t one = 1u;
+          const uint32_t at = static_cast<uint32_t>(
+              reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint32_t *)(cntL + q)));
+          asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(pos) : "v"(at), "v"(one) : "memory");
           if (pos < static_cast<uint32_t>(kB)) {
             gb[q * kB + pos] = static_cast<uint64_t>(__float_as_uint(d)) | (static_cast<uint64_t>(rid) << 32);
             ne |= 1u << r;
@@ -1511,14 +1544,16 @@ __device__ float exact_l2(const FlatParams &p, const float *q, uint32_t id, int 
 // |C~ - C| <= (2^-10 + 2^-22) |q||b| + (1 + 2^-11) sqrt(K) (a_b |q| + a_q |b|) + K a_q a_b,
 // twice that on the distance (gam x 1.01 for the slightly larger rounded operands).  A query whose
 // scale-back 2^-(s+t) would leave f32's range is not provable: ok = false.
-__device__ __forceinline__ float shortlist_eps(const FlatParams &p, float qn, float qmax, float &gam, bool &ok) {
+__device__ __forceinline__ float shortlist_eps(const FlatParams &p, float qn, float qmax, float &gam, bool &ok,
+                                              uint64_t qi) {
   const float qnorm = sqrtf(qn);
   const float bmax = p.max_norm;
   ok = true;
   gam = 2.0f * static_cast<float>(p.k_acc) * 5.9604645e-8f * (p.split ? 3.1f : (p.single ? 1.01f : 1.0f));
   float eps = gam * (qn + bmax * bmax + 2.0f * qnorm * bmax);
   if (p.single) {
-    const int t = f16_exp(qmax);
+    // the scale the scan used: the single-role scan's is per wave of 32 queries (p.tiles_qexp)
+    const int t = p.tiles_qexp ? p.tiles_qexp[qi] : f16_exp(qmax);
     if (abs(p.base_exp + t) > kF16MaxExp || !(qn < 3.0e38f)) ok = false;
     const float ab = ldexpf(1.0f, -14 - p.base_exp), aq = ldexpf(1.0f, -14 - t);
     const float rk = sqrtf(static_cast<float>(p.k_acc));
@@ -1613,7 +1648,7 @@ __global__ void __launch_bounds__(64) flat_merge_kernel(FlatParams p) {
     }
     float gam = 0.f;
     bool ok = true;
-    const float eps = shortlist_eps(p, qn, qmax, gam, ok);
+    const float eps = shortlist_eps(p, qn, qmax, gam, ok, qi);
     const bool exact = ok && (kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX);
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     wave_fence();
@@ -1779,7 +1814,7 @@ __global__ void __launch_bounds__(64) flat_merge_big_kernel(FlatParams p) {
       if ((p.k - 1) / 64 == static_cast<uint32_t>(r)) kth_d = __shfl(E[r], (p.k - 1) & 63);
     float gam = 0.f;
     bool ok = true;
-    const float eps = shortlist_eps(p, qn, qmax, gam, ok);
+    const float eps = shortlist_eps(p, qn, qmax, gam, ok, qi);
     const bool exact = ok && (kth_d * (1.0f + gam) < cutoff + qn - eps || cutoff == FLT_MAX);
     if (lane == 0 && p.flags) p.flags[qi] = exact ? 0u : 1u;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -128,9 +128,10 @@ def test_flat_exact_large_k(native, orc, n, d, nq, k):
 
 
 def test_flat_f16_query_scale_out_of_range(native, orc, flat_mode):
-    """Queries whose f16 scale-back 2^-(s+t) would leave f32's range (1e-30-sized queries against
-    rows of norm ~6) cannot be proven by the single pass: the merge flags them, more than 1 % flagged
-    reruns the launch with the split, and the answer is exact."""
+    """Queries whose own f16 scale-back 2^-(s+t) would leave f32's range (1e-30-sized queries against
+    rows of norm ~6): with per-query scales (the warp-specialised scan) the merge flags them and more
+    than 1 % flagged reruns the launch with the split; with the single-role scan's per-wave scale
+    they are proven as they are.  The answer is exact either way."""
     rng = np.random.default_rng(17)
     base = np.ascontiguousarray(rng.random((4000, 64), dtype=np.float32))
     q = np.ascontiguousarray(rng.random((20, 64), dtype=np.float32))
@@ -141,8 +142,10 @@ def test_flat_f16_query_scale_out_of_range(native, orc, flat_mode):
     ref_i, ref_d = _exact(orc, base, q, 10)
     assert np.array_equal(ids, ref_i)
     assert np.array_equal(dists.view(np.uint32), ref_d.view(np.uint32))
-    if flat_mode == "f16":  # five of twenty flagged: the launch reran with the split
+    if flat_mode == "f16-ws":  # per-query scales: five of twenty flagged, the launch reran with the split
         assert dev.flat_contraction() == 1
+    # the single-role scan scales each wave of 32 queries by its largest element, so the tiny
+    # queries' operands flush to zero and the bound's absolute term (2^-14-t |b|) proves them
 
 
 def test_flat_rejects_unsupported(native):
