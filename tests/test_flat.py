@@ -332,3 +332,40 @@ def test_flat_tile_records_follow_updates(orc, flat_mode):
         flat(rows, valid)
     finally:
         lib.alaya_index_destroy(ix)
+
+
+@pytest.fixture(scope="module")
+def flat_many(orc):
+    rng = np.random.default_rng(8448)
+    base = rng.random((100_000, 128), dtype=np.float32)
+    q = rng.random((8448, 128), dtype=np.float32)
+    ref_i, _ = orc.exact_gt(base, q, 10, num_threads=16)
+    return base, q, ref_i
+
+
+def test_flat_many_query_groups(native, orc, flat_many, flat_mode):
+    """More query groups than the chip has block slots at 8 chunks (8,448 queries = 33 groups of
+    256 in the single-role scan): the chunk count is chosen to fill whole rounds of the CUs and the
+    last group is partial; the prescan runs in the -prescan modes only (3,125 records is below its
+    default size).  The oracle's find_exact_gt orders equal distances by std::sort, the device by
+    id, so a row whose ids differ must hold the same distances, bit for bit (ties); every returned
+    distance is the oracle's distance of that row."""
+    base, q, ref_i = flat_many
+    dev = native.DeviceIndex(0)
+    dev.set_base(base, 0)
+    ids, dists, redo = dev.flat_search(q, 10)
+    assert redo == 0
+    lib = orc.lib()
+
+    def d_of(a, row_ids):
+        qa = np.ascontiguousarray(q[a])
+        return np.array([lib.orc_l2_f32(orc._ptr(qa), orc._ptr(base[i]), 128) for i in row_ids], np.float32)
+
+    diff = np.nonzero((ids != ref_i.astype(np.uint32)).any(1))[0]
+    assert len(diff) <= len(q) // 100, len(diff)  # ties only
+    for a in diff:
+        got, ref = d_of(a, ids[a]), d_of(a, ref_i[a])
+        assert np.array_equal(got.view(np.uint32), dists[a].view(np.uint32)), a
+        assert np.array_equal(np.sort(got).view(np.uint32), np.sort(ref).view(np.uint32)), (a, ids[a], ref_i[a])
+    for a in range(0, len(q), 997):
+        assert np.array_equal(d_of(a, ids[a]).view(np.uint32), dists[a].view(np.uint32)), a
