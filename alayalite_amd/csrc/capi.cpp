@@ -624,17 +624,17 @@ void flat_prescan(alaya_index *ix, alaya_amd::FlatParams &p, int *blocks, hipStr
   const uint64_t step = env ? std::strtoull(env, nullptr, 10) : 0;
   if (p.tiles != nullptr) {
     // The single-role scan's prescan: group minima over a sample of whole tile records (every S-th;
-    // default S = records / 2048, on when the base has >= 8192 records, ALAYA_FLAT_PRESCAN=S forces S,
+    // default S = records / 4096, on when the base has >= 8192 records, ALAYA_FLAT_PRESCAN=S forces S,
     // 1 turns it off), one block per (query group, group of sampled records); the 32nd smallest
     // of a query's group minima is its starting threshold (flat_group_threshold_kernel).
     const uint64_t nt = p.n_scan_tiles;
     const char *genv = std::getenv("ALAYA_FLAT_PRESCAN_GROUPS");  // diagnostics: groups (default 64)
-    const char *senv = std::getenv("ALAYA_FLAT_PRESCAN_SAMPLE");  // diagnostics: sampled records (2048)
-    const uint64_t want_sample = senv ? std::max<uint64_t>(32, std::strtoull(senv, nullptr, 10)) : 2048;
-    uint64_t S = env ? step : (nt >= 4 * want_sample ? nt / want_sample : 0);
+    const char *senv = std::getenv("ALAYA_FLAT_PRESCAN_SAMPLE");  // diagnostics: sampled records (4096)
+    const uint64_t want_sample = senv ? std::max<uint64_t>(32, std::strtoull(senv, nullptr, 10)) : 4096;
+    uint64_t S = env ? step : (nt >= 2 * want_sample ? nt / want_sample : 0);
     if (S < 1 || (env && S < 2)) return;
     const uint64_t sample = (nt + S - 1) / S;
-    // groups of >= 1 sampled record (32 at the defaults); the minima (groups x nq floats) fit the
+    // groups of >= 1 sampled record (64+ at the defaults); the minima (groups x nq floats) fit the
     // candidate buffers (n_chunks >= 8 lists of 32 per query)
     const uint64_t want_groups = genv ? std::strtoull(genv, nullptr, 10) : 64;
     const uint64_t groups = std::min<uint64_t>(std::min<uint64_t>(256, want_groups), sample) / 8 * 8;
