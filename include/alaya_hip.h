@@ -216,7 +216,10 @@ int alaya_index_shard_search_sq8_device(alaya_index *ix, const float *d_queries,
  * scaled operands (rows of <= 224 floats) or a bf16 hi/lo split (3 bf16 MFMAs; wider rows), each
  * error bounded and folded into the proof below (alaya_index_flat_last_contraction; environment
  * ALAYA_FLAT_CONTRACTION selects one, ALAYA_FLAT_F32=1 the f32 MFMA form); rows wider than 224
- * floats are scanned in K slabs.  The shortlist (32 per row chunk,
+ * floats are scanned in K slabs.  The single-pass scan reads f16 tile records of the rows that the
+ * index builds at its first flat search and keeps (K/16 KB + 256 B per 32 rows: 264.5 MB for
+ * 1M x 128), rebuilding them after any change to the rows, their count or the validity bitmap;
+ * a prescan over a sample of them seeds every query's threshold.  The shortlist (32 per row chunk,
  * folded into a 128/256-entry list for k > 24) is rescored with the exact device metric
  * (l2_sqr_avx2 order) and sorted by (distance, id).  A query whose shortlist cannot be proven to
  * hold the exact top-k (error bound in flat_kernels.hip) is flagged; the host API recomputes it
