@@ -59,7 +59,10 @@ def _exact(orc, base, q, k):
 
 
 @pytest.mark.parametrize("n,d,nq", [(5000, 128, 37), (3000, 32, 130), (2500, 100, 9), (4000, 200, 64),
-                                    (2000, 224, 5), (777, 64, 300)])
+                                    (2000, 224, 5), (777, 64, 300),
+                                    # the remaining narrow strides (96, 160, 192 floats): every
+                                    # instantiation of the single-role and warp-specialised scans
+                                    (3000, 96, 33), (2600, 150, 21), (2400, 180, 70)])
 def test_flat_exact(native, orc, flat_mode, n, d, nq):
     rng = np.random.default_rng(n + d)
     base = np.ascontiguousarray(rng.random((n, d), dtype=np.float32))
